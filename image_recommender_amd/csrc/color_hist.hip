@@ -1,0 +1,197 @@
+// color_hist.hip — per-image RGB histogram on gfx950 (row A15 of SURVEY.md §8a).
+//
+// Restates /root/reference/vector_scripts/create_color_vector.py:46-51 (cv2.calcHist with
+// `bins` uniform bins over [0, 256) per channel, R|G|B concatenated, L2-normalised) for a batch of
+// decoded images.  HBM-bound byte work: one workgroup per image streams the image's bytes with
+// 16-B loads; every thread counts into its OWN column of an LDS histogram laid out
+// [bin][thread] (u32, ds_add_u32), so no two lanes ever touch the same word and the 32 lanes of a
+// half-wave always hit 32 different banks — no contention however skewed the image is.  The
+// per-thread columns are then summed by wave reductions, normalised and written out.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/imgrec_color.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ void __launch_bounds__(NT)
+color_hist_kernel(const uint8_t* __restrict__ pix, const int64_t* __restrict__ offsets,
+                  const int64_t* __restrict__ npix, int bins, float* __restrict__ out,
+                  uint32_t* __restrict__ counts) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hist[];   // [3*bins][NT]
+    const int tid = threadIdx.x;
+    const int nb = 3 * bins;
+    for (int i = tid; i < nb * NT; i += NT) hist[i] = 0u;
+    __syncthreads();
+
+    const int64_t img = blockIdx.x;
+    const int64_t off = offsets[img];
+    const int64_t nbytes = 3 * npix[img];
+    const uint8_t* base = pix + off;
+
+    auto count = [&](int c, uint32_t v) {
+        const int b = (int)((v * (uint32_t)bins) >> 8);
+        atomicAdd(&hist[(c * bins + b) * NT + tid], 1u);
+    };
+
+    // head: bytes before the first 16-B aligned address
+    const int64_t head = std::min<int64_t>(nbytes, (int64_t)((16 - ((uintptr_t)base & 15)) & 15));
+    if (tid < head) count((int)(tid % 3), base[tid]);
+    // aligned body, 16 bytes per thread per iteration
+    const int64_t body = (nbytes - head) & ~(int64_t)15;
+    const uint4* vb = reinterpret_cast<const uint4*>(base + head);
+    const int64_t nvec = body >> 4;
+    // channel of the first byte of vector i is (head + 16 i) % 3; a stride of NT vectors moves it
+    // by 16 * NT = 4096 = 1 (mod 3)
+    int cv = (int)((head + (int64_t)tid * 16) % 3);
+    for (int64_t i = tid; i < nvec; i += NT, cv = (cv == 2) ? 0 : cv + 1) {
+        const uint4 w = vb[i];
+        int c = cv;
+        const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                count(c, (words[q] >> (8 * j)) & 0xffu);
+                c = (c == 2) ? 0 : c + 1;
+            }
+        }
+    }
+    // tail
+    const int64_t t0 = head + body;
+    if (t0 + tid < nbytes) count((int)((t0 + tid) % 3), base[t0 + tid]);
+    __syncthreads();
+
+    // column sums: wave w reduces bins w, w+4, ...; lane reads 4 consecutive-thread entries
+    __shared__ float tot[3 * COLOR_HIST_MAX_BINS];
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int b = wave; b < nb; b += NT / 64) {
+        const uint32_t* row = hist + b * NT;
+        uint32_t s = row[lane] + row[lane + 64] + row[lane + 128] + row[lane + 192];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (lane == 0) {
+            tot[b] = (float)s;
+            if (counts) counts[img * nb + b] = s;
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // L2 norm of the float32 count vector (np.linalg.norm on the calcHist output)
+        float ss = 0.f;
+        for (int b = lane; b < nb; b += 64) ss = fmaf(tot[b], tot[b], ss);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+        const float l2 = sqrtf(ss);
+        for (int b = lane; b < nb; b += 64) out[img * nb + b] = (l2 != 0.f) ? tot[b] / l2 : tot[b];
+    }
+}
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* color_hist_last_error(void) { return g_err.c_str(); }
+
+int color_hist_device(const uint8_t* pixels, const int64_t* offsets, const int64_t* npix,
+                      int64_t n_images, int bins, float* out, uint32_t* counts, void* stream) {
+    if (n_images < 0 || bins < 1 || bins > COLOR_HIST_MAX_BINS) {
+        set_err("bad arguments (n_images=%lld bins=%d, bins must be in [1,%d])",
+                (long long)n_images, bins, COLOR_HIST_MAX_BINS);
+        return -1;
+    }
+    if (n_images == 0) return 0;
+    if (!pixels || !offsets || !npix || !out) {
+        set_err("NULL pointer");
+        return -1;
+    }
+    const size_t lds = (size_t)3 * bins * NT * sizeof(uint32_t);
+    hipLaunchKernelGGL(color_hist_kernel, dim3((unsigned)n_images), dim3(NT), lds,
+                       (hipStream_t)stream, pixels, offsets, npix, bins, out, counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_err("color_hist_kernel launch failed: %s", hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
+
+int color_hist_host(const uint8_t* pixels, int64_t total_bytes, const int64_t* offsets,
+                    const int64_t* npix, int64_t n_images, int bins, int device, float* out,
+                    uint32_t* counts) {
+    if (n_images == 0) return 0;
+    if (total_bytes < 0 || !pixels || !offsets || !npix || !out || n_images < 0) {
+        set_err("bad arguments");
+        return -1;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        set_err("no HIP device visible");
+        return -5;
+    }
+    for (int64_t i = 0; i < n_images; ++i) {
+        if (offsets[i] < 0 || npix[i] < 0 || offsets[i] + 3 * npix[i] > total_bytes) {
+            set_err("image %lld lies outside the pixel buffer", (long long)i);
+            return -1;
+        }
+    }
+    int old = -1;
+    (void)hipGetDevice(&old);
+    if (device >= 0) (void)hipSetDevice(device);
+    uint8_t* dp = nullptr;
+    int64_t* doff = nullptr;
+    int64_t* dn = nullptr;
+    float* dout = nullptr;
+    uint32_t* dc = nullptr;
+    const int nb = 3 * bins;
+    int rc = 0;
+    hipError_t e = hipMalloc((void**)&dp, (size_t)std::max<int64_t>(total_bytes, 16));
+    if (e == hipSuccess) e = hipMalloc((void**)&doff, (size_t)n_images * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&dn, (size_t)n_images * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, (size_t)n_images * nb * 4);
+    if (e == hipSuccess && counts) e = hipMalloc((void**)&dc, (size_t)n_images * nb * 4);
+    if (e == hipSuccess) e = hipMemcpy(dp, pixels, (size_t)total_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(doff, offsets, (size_t)n_images * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dn, npix, (size_t)n_images * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_err("staging failed: %s", hipGetErrorString(e));
+        rc = -2;
+    } else {
+        rc = color_hist_device(dp, doff, dn, n_images, bins, dout, dc, nullptr);
+        if (rc == 0) {
+            e = hipMemcpy(out, dout, (size_t)n_images * nb * 4, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && counts)
+                e = hipMemcpy(counts, dc, (size_t)n_images * nb * 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                set_err("copy-back failed: %s", hipGetErrorString(e));
+                rc = -2;
+            }
+        }
+    }
+    for (void* p : {(void*)dp, (void*)doff, (void*)dn, (void*)dout, (void*)dc})
+        if (p) (void)hipFree(p);
+    if (old >= 0) (void)hipSetDevice(old);
+    return rc;
+}
+
+}  // extern "C"

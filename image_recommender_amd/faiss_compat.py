@@ -1,0 +1,258 @@
+"""faiss-compatible index objects backed by the MI355X k-NN kernels (libimgrec.so).
+
+This module is the drop-in boundary of SURVEY.md §8b: it provides exactly the faiss Python
+surface that the reference's hot path touches, so ``import faiss`` in the reference can be
+replaced by ``from image_recommender_amd import faiss_compat as faiss``:
+
+================================  =================================================================
+reference call                    where
+================================  =================================================================
+``faiss.IndexHNSWFlat(d, M)``     main/create_index.py:219, 230 (+ ``.hnsw.efConstruction/
+                                  efSearch`` sets at :220-221, 231-232)
+``faiss.IndexIVFPQ(q,d,nl,m,nb)`` main/create_index.py:226
+``index.is_trained / train``      main/create_index.py:296-298
+``index.add(arr)``                main/create_index.py:311
+``index.ntotal``                  main/create_index.py:321, main/search_from_image.py:340
+``faiss.write_index``             main/create_index.py:320
+``faiss.read_index``              main/search_from_image.py:339
+``faiss.normalize_L2``            main/search_from_image.py:322
+``index.search(q, k)``            main/search_from_image.py:247, Analytics/rt_Search.py:63
+================================  =================================================================
+
+Semantics: every index class here is an EXACT flat index (the north_star parity target is
+``IndexFlatL2``).  ``IndexHNSWFlat`` and ``IndexIVFPQ`` keep their constructor signatures and
+attributes (``hnsw.efSearch``, ``nprobe``, ``nlist``, ...) so the reference code runs unchanged,
+but they search exactly; their results are therefore the ones the reference's approximate index
+approximates.  Results follow faiss conventions: ``D`` float32 (n, k), ``I`` int64 (n, k), rows
+sorted best-first, missing neighbours as label -1 with distance FLT_MAX (L2) / -FLT_MAX (IP).
+Exact ties are broken by the smaller label.
+
+All arithmetic runs in the HIP kernels; there is no CPU fallback (``NativeLibraryError`` when the
+library is missing, ``KnnError`` with the C-ABI message on any failure).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from types import SimpleNamespace
+
+import numpy as np
+
+from . import _lib
+from ._lib import KNN_MAX_K, KnnError
+
+METRIC_INNER_PRODUCT = 0
+METRIC_L2 = 1
+METRIC_COSINE = 2   # extension: rows and queries L2-normalised on entry, then inner product
+
+_METRIC_TO_KNN = {METRIC_L2: _lib.KNN_METRIC_L2, METRIC_INNER_PRODUCT: _lib.KNN_METRIC_IP,
+                  METRIC_COSINE: _lib.KNN_METRIC_COSINE}
+_KNN_TO_METRIC = {v: k for k, v in _METRIC_TO_KNN.items()}
+
+
+def _as_matrix(x, d: int, what: str) -> np.ndarray:
+    """faiss's swig replacement_* wrappers: ``n, d = x.shape; x = ascontiguousarray(x, float32)``."""
+    x = np.asarray(x)
+    if x.ndim != 2:
+        raise ValueError(f"{what}: expected a 2-D array, got shape {x.shape}")
+    if x.shape[1] != d:
+        raise ValueError(f"{what}: array has {x.shape[1]} columns, index dimension is {d}")
+    return np.ascontiguousarray(x, dtype=np.float32)
+
+
+def _ptr(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+class Index:
+    """Exact flat index on one HIP device (faiss.IndexFlat semantics)."""
+
+    def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1):
+        if metric not in _METRIC_TO_KNN:
+            raise ValueError(f"unsupported metric {metric}")
+        self._h = None
+        lib = _lib.load()
+        h = C.c_void_p()
+        _lib.check(lib.knn_create(int(d), _METRIC_TO_KNN[metric], int(device), C.byref(h)),
+                   "knn_create")
+        self._h = h
+        self.d = int(d)
+        self.metric_type = metric
+        self.verbose = False
+
+    @classmethod
+    def _wrap(cls, handle: C.c_void_p) -> "Index":
+        obj = cls.__new__(cls)
+        lib = _lib.load()
+        obj._h = handle
+        obj.d = lib.knn_dim(handle)
+        obj.metric_type = _KNN_TO_METRIC[lib.knn_metric(handle)]
+        obj.verbose = False
+        return obj
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        lib = getattr(_lib, "_lib", None) if _lib is not None else None
+        if h is not None and lib is not None:
+            lib.knn_free(h)
+            self._h = None
+
+    # ---- faiss attributes -------------------------------------------------------------------
+    @property
+    def ntotal(self) -> int:
+        return int(_lib.load().knn_ntotal(self._h))
+
+    @property
+    def is_trained(self) -> bool:
+        return bool(_lib.load().knn_is_trained(self._h))
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # ---- faiss methods ----------------------------------------------------------------------
+    def train(self, x) -> None:
+        x = _as_matrix(x, self.d, "train")
+        _lib.check(_lib.load().knn_train(self._h, _ptr(x), x.shape[0]), "knn_train")
+
+    def add(self, x) -> None:
+        x = _as_matrix(x, self.d, "add")
+        if not self.is_trained:
+            raise RuntimeError("Error in add: index is not trained (call train first)")
+        _lib.check(_lib.load().knn_add(self._h, _ptr(x), x.shape[0]), "knn_add")
+
+    def search(self, x, k: int, *, D=None, I=None):
+        x = _as_matrix(x, self.d, "search")
+        k = int(k)
+        if k <= 0:
+            raise ValueError("k must be positive")
+        if k > KNN_MAX_K:
+            raise NotImplementedError(f"k={k} exceeds the fused top-k limit of {KNN_MAX_K}")
+        n = x.shape[0]
+        D = np.empty((n, k), dtype=np.float32) if D is None else D
+        I = np.empty((n, k), dtype=np.int64) if I is None else I
+        if D.shape != (n, k) or I.shape != (n, k) or D.dtype != np.float32 or I.dtype != np.int64 \
+                or not D.flags.c_contiguous or not I.flags.c_contiguous:
+            raise ValueError("D/I must be C-contiguous float32/int64 arrays of shape (n, k)")
+        if n:
+            _lib.check(_lib.load().knn_search(self._h, _ptr(x), n, k, _ptr(D), _ptr(I)),
+                       "knn_search")
+        return D, I
+
+    def reset(self) -> None:
+        _lib.check(_lib.load().knn_reset(self._h), "knn_reset")
+
+    def reconstruct_n(self, i0: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.ntotal - i0 if n is None else n
+        out = np.empty((n, self.d), dtype=np.float32)
+        _lib.check(_lib.load().knn_reconstruct_n(self._h, int(i0), int(n), _ptr(out)),
+                   "knn_reconstruct_n")
+        return out
+
+    def reconstruct(self, key: int) -> np.ndarray:
+        return self.reconstruct_n(int(key), 1)[0]
+
+    # ---- device-resident entry points (multi-GPU shards, bench) ---------------------------------
+    def add_device(self, x_ptr: int, n: int, stream: int = 0) -> None:
+        _lib.check(_lib.load().knn_add_device(self._h, C.c_void_p(x_ptr), int(n),
+                                              C.c_void_p(stream or None)), "knn_add_device")
+
+    def search_device(self, q_ptr: int, nq: int, k: int, d_ptr: int, i_ptr: int,
+                      stream: int = 0) -> None:
+        _lib.check(_lib.load().knn_search_device(self._h, C.c_void_p(q_ptr), int(nq), int(k),
+                                                 C.c_void_p(d_ptr), C.c_void_p(i_ptr),
+                                                 C.c_void_p(stream or None)), "knn_search_device")
+
+    def set_id_offset(self, off: int) -> None:
+        _lib.check(_lib.load().knn_set_id_offset(self._h, int(off)), "knn_set_id_offset")
+
+    def reserve(self, n: int) -> None:
+        _lib.check(_lib.load().knn_reserve(self._h, int(n)), "knn_reserve")
+
+
+class IndexFlat(Index):
+    def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1):
+        super().__init__(d, metric, device)
+
+
+class IndexFlatL2(Index):
+    def __init__(self, d: int, device: int = -1):
+        super().__init__(d, METRIC_L2, device)
+
+
+class IndexFlatIP(Index):
+    def __init__(self, d: int, device: int = -1):
+        super().__init__(d, METRIC_INNER_PRODUCT, device)
+
+
+class IndexHNSWFlat(IndexFlatL2):
+    """Constructor-compatible with ``faiss.IndexHNSWFlat(d, M[, metric])``; searches exactly.
+
+    ``hnsw.efConstruction`` / ``hnsw.efSearch`` / ``hnsw.max_level`` are accepted and recorded
+    (main/create_index.py:220-221, 231-232) but have no effect on an exact search.
+    """
+
+    def __init__(self, d: int, M: int = 32, metric: int = METRIC_L2, device: int = -1):
+        Index.__init__(self, d, metric, device)
+        self.hnsw = SimpleNamespace(efConstruction=40, efSearch=16, max_level=0, M=int(M))
+
+
+class IndexIVFPQ(Index):
+    """Constructor-compatible with ``faiss.IndexIVFPQ(quantizer, d, nlist, m, nbits)``
+    (main/create_index.py:226); searches exactly (nprobe is recorded, not used).
+
+    Like faiss it starts untrained, so the reference's ``if not index.is_trained: train`` runs.
+    """
+
+    def __init__(self, quantizer, d: int, nlist: int, m: int, nbits: int = 8,
+                 metric: int = METRIC_L2, device: int = -1):
+        if d % m != 0:
+            raise ValueError(f"IndexIVFPQ: d={d} is not a multiple of m={m}")
+        Index.__init__(self, d, metric, device)
+        self.quantizer = quantizer
+        self.nlist, self.pq_m, self.pq_nbits = int(nlist), int(m), int(nbits)
+        self.nprobe = 1
+        self._trained = False
+
+    @property
+    def is_trained(self) -> bool:
+        return self._trained
+
+    def train(self, x) -> None:
+        super().train(x)
+        self._trained = True
+
+
+def normalize_L2(x: np.ndarray) -> None:
+    """In-place row L2 normalisation (faiss.normalize_L2; rows with norm 0 are left unchanged)."""
+    if not isinstance(x, np.ndarray) or x.dtype != np.float32 or not x.flags.c_contiguous:
+        raise TypeError("normalize_L2 expects a C-contiguous float32 numpy array")
+    if x.ndim == 1:
+        n, d = 1, x.shape[0]
+    elif x.ndim == 2:
+        n, d = x.shape
+    else:
+        raise ValueError("normalize_L2 expects a 1-D or 2-D array")
+    if n and d:
+        _lib.check(_lib.load().knn_normalize_L2(_ptr(x), n, d), "knn_normalize_L2")
+
+
+def write_index(index: Index, fname) -> None:
+    """Write in faiss's IndexFlat layout (fourcc IxF2 / IxFI), readable by faiss.read_index."""
+    _lib.check(_lib.load().knn_write(index.handle, str(fname).encode()), "knn_write")
+
+
+def read_index(fname, device: int = -1) -> Index:
+    h = C.c_void_p()
+    rc = _lib.load().knn_read(str(fname).encode(), int(device), C.byref(h))
+    if rc < 0:
+        # faiss raises RuntimeError from read_index; the recommender logs and returns None
+        raise KnnError(f"read_index({fname}) failed (code {rc}): {_lib.last_error()}")
+    m = _lib.load().knn_metric(h)
+    cls = IndexFlatL2 if m == _lib.KNN_METRIC_L2 else (IndexFlatIP if m == _lib.KNN_METRIC_IP
+                                                       else IndexFlat)
+    return cls._wrap(h)
+
+
+__all__ = ["Index", "IndexFlat", "IndexFlatL2", "IndexFlatIP", "IndexHNSWFlat", "IndexIVFPQ",
+           "normalize_L2", "read_index", "write_index", "METRIC_L2", "METRIC_INNER_PRODUCT",
+           "METRIC_COSINE", "KnnError"]

@@ -1,0 +1,127 @@
+/*
+ * imgrec_knn.h — C ABI of the MI355X exact k-NN index (the image_recommender hot path).
+ *
+ * This is the drop-in boundary for the faiss calls the reference makes on its search/index path
+ * (SURVEY.md §8b).  Every entry point below replaces one faiss call site of the reference:
+ *
+ *   knn_create(d, KNN_METRIC_L2, ...)   faiss.IndexFlatL2(d) — the parity target named by north_star; the
+ *                                        reference default IndexIVFPQ(IndexHNSWFlat(d,32),d,2048,m,12) is
+ *                                        built at /root/reference/main/create_index.py:218-228
+ *   knn_train                            index.train(train_vecs)       main/create_index.py:296-299
+ *   knn_add / knn_add_device             index.add(arr)                main/create_index.py:311
+ *   knn_search / knn_search_device       index.search(query_vec, k)    main/search_from_image.py:247,
+ *                                                                      Analytics/rt_Search.py:63
+ *   knn_ntotal / knn_dim                 index.ntotal / index.d        main/search_from_image.py:340,
+ *                                                                      main/create_index.py:321
+ *   knn_write                            faiss.write_index(index, f)   main/create_index.py:320
+ *   knn_read                             faiss.read_index(f)           main/search_from_image.py:339
+ *   knn_normalize_L2                     faiss.normalize_L2(x)         main/search_from_image.py:322
+ *   knn_merge_device                     (new) per-shard top-k merge after the RCCL all-gather (§8e)
+ *
+ * Conventions
+ *   - All functions return 0 on success and a negative KNN_E* code on failure; the message of the
+ *     last failure on the calling thread is returned by knn_last_error().
+ *   - Host-pointer functions (knn_add, knn_search, knn_write, ...) synchronise before returning.
+ *     *_device functions take device pointers and a hipStream_t (passed as void*; NULL = the
+ *     index's own stream), enqueue asynchronously and never synchronise or allocate when the
+ *     workspace is already large enough (so a caller may capture them into a hipGraph).
+ *   - Vectors are row-major float32, n rows × d.  Labels are int64.  Result rows are sorted by
+ *     ascending distance (L2) or descending inner product (IP/COSINE); exact ties are broken by the
+ *     smaller label.  When fewer than k vectors exist, the tail of a result row holds label -1 and
+ *     distance FLT_MAX (L2) or -FLT_MAX (IP/COSINE), as faiss's heaps do.
+ *   - L2 distances are squared L2, evaluated as (|q|^2 + |x|^2) - 2 q.x and clamped at 0, as in
+ *     faiss's exhaustive_L2sqr_blas.
+ */
+#ifndef IMGREC_KNN_H
+#define IMGREC_KNN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct knn_index knn_index_t;
+
+enum knn_metric {
+    KNN_METRIC_IP = 0,     /* faiss METRIC_INNER_PRODUCT (IndexFlatIP) */
+    KNN_METRIC_L2 = 1,     /* faiss METRIC_L2 (IndexFlatL2) */
+    KNN_METRIC_COSINE = 2  /* rows and queries L2-normalised on entry, then IP */
+};
+
+enum knn_error {
+    KNN_OK = 0,
+    KNN_EINVAL = -1,   /* bad argument (d <= 0, k <= 0, NULL pointer, unsupported k, ...) */
+    KNN_EHIP = -2,     /* HIP runtime error */
+    KNN_ENOMEM = -3,   /* device allocation failed */
+    KNN_EIO = -4,      /* file could not be read/written or has a bad layout */
+    KNN_ENOSYS = -5    /* not supported (e.g. no GPU visible) */
+};
+
+/* Largest k one search can return (the fused top-k keeps per-lane lists of this length). */
+#define KNN_MAX_K 32
+
+/* Create an empty index of dimension d on HIP device `device` (-1 = current device). */
+int knn_create(int d, int metric, int device, knn_index_t** out);
+int knn_free(knn_index_t* index);
+
+int knn_dim(const knn_index_t* index);
+int knn_metric(const knn_index_t* index);
+int64_t knn_ntotal(const knn_index_t* index);
+int knn_is_trained(const knn_index_t* index);
+
+/* Labels returned by search are (row offset + id_offset); a row shard sets its global base here. */
+int knn_set_id_offset(knn_index_t* index, int64_t id_offset);
+
+/* Flat index: training only marks the index trained (faiss IndexFlat is always trained). */
+int knn_train(knn_index_t* index, const float* x, int64_t n);
+
+/* Append n rows; ids are implicitly ntotal .. ntotal+n-1 (faiss Index::add). */
+int knn_add(knn_index_t* index, const float* x_host, int64_t n);
+int knn_add_device(knn_index_t* index, const float* x_dev, int64_t n, void* stream);
+/* Pre-size the corpus buffer for n rows (avoids regrowth copies during streamed adds). */
+int knn_reserve(knn_index_t* index, int64_t n);
+int knn_reset(knn_index_t* index);
+
+/* Copy rows [i0, i0+n) back to the host as stored (normalised for COSINE). */
+int knn_reconstruct_n(const knn_index_t* index, int64_t i0, int64_t n, float* x_host);
+
+/* k nearest neighbours of nq queries.  D, I: nq*k, row-major. */
+int knn_search(knn_index_t* index, const float* q_host, int64_t nq, int k,
+               float* D_host, int64_t* I_host);
+int knn_search_device(knn_index_t* index, const float* q_dev, int64_t nq, int k,
+                      float* D_dev, int64_t* I_dev, void* stream);
+
+/* Merge nlists candidate lists per query into the top k.  cand_D/cand_I are laid out
+ * [nlists][nq][kin] (the layout of an all-gather of per-shard [nq][kin] results); entries with
+ * label -1 are ignored.  Output nq*k, same ordering/padding rules as knn_search. */
+int knn_merge_device(const float* cand_D, const int64_t* cand_I, int nlists, int64_t nq, int kin,
+                     int k, int metric, float* D_dev, int64_t* I_dev, void* stream);
+
+/* faiss IndexFlat on-disk layout ("IxF2" for L2, "IxFI" for IP/COSINE). */
+int knn_write(const knn_index_t* index, const char* path);
+int knn_read(const char* path, int device, knn_index_t** out);
+
+/* In-place row normalisation of a host array (faiss.normalize_L2: rows with norm 0 unchanged). */
+int knn_normalize_L2(float* x_host, int64_t n, int d);
+
+/* Kernel timing for the live roofline figure in bench.py.  While enabled, every search records a
+ * HIP event pair around its fused distance+top-k launch, on the stream that launch uses.
+ * knn_kernel_time waits for the recorded events, returns the summed duration (ms) and launch
+ * count since the last call, and clears them. */
+int knn_set_timing(knn_index_t* index, int enable);
+int knn_kernel_time(knn_index_t* index, double* total_ms, int* launches);
+
+/* Launch geometry chosen for a search of nq queries (for reports): workgroup tile rows/queries,
+ * row splits and workgroup count. */
+int knn_plan(const knn_index_t* index, int64_t nq, int k, int* tile_rows, int* tile_queries,
+             int* splits, int* workgroups);
+
+const char* knn_last_error(void);
+const char* knn_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IMGREC_KNN_H */
