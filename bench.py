@@ -1,0 +1,334 @@
+#!/usr/bin/env python3
+"""Benchmark of the exact k-NN hot path on MI355X (BASELINE.json metric).
+
+metric: "k-NN queries/sec + recall@10 on 1M concat vectors at 1/2/4/8 MI355X".
+Default workload = SURVEY.md §8d config 3: N = 1,000,000 rows of D = 1968 = 48 (colour, |N(0,1)|)
+| 128 (SIFT-VLAD, mixture) | 1792 (DreamSim, mixture), every part L2-normalised (the reference's
+stored layout, |x|^2 = 3), queries L2-normalised after concatenation (reference
+main/search_from_image.py:305-322), squared-L2 ranking (== cosine ranking on this layout), k = 10,
+batches of Q = 1024 queries.  Data are synthetic and generated on device, block-seeded so every
+sharding sees the same rows.
+
+A step = one batch of Q queries searched against the whole corpus: on N GPUs each rank searches its
+contiguous row shard (fused distance + top-k kernel), the per-shard (Q, k) results are all-gathered
+over RCCL and merged (strong scaling: the corpus is fixed, per-GPU rows shrink as N grows).
+
+Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1) prints ONE JSON line
+on rank 0.  `value` = Q*K / max-over-ranks wall time of the K steps, inputs resident in HBM.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (spec)
+BLOCK = 16384                    # rows per generation block (the seed unit)
+
+CONFIGS = {
+    2: dict(name="cfg2: 1M x 768 DreamSim-only, L2", rows=1_000_000, parts=(768,), centres=(1000,)),
+    3: dict(name="cfg3: 1M x 1968 concat(color48|sift128|dreamsim1792), cosine ranking",
+            rows=1_000_000, parts=(48, 128, 1792), centres=(0, 256, 1000)),
+    4: dict(name="cfg4: 10M x 1968 concat, row-sharded", rows=10_000_000, parts=(48, 128, 1792),
+            centres=(0, 256, 1000)),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=None, help="override corpus rows (total)")
+    ap.add_argument("--nq", type=int, default=1024, help="queries per batch")
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--gt-queries", type=int, default=128, help="queries checked for recall@k")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
+    ap.add_argument("--single-query-steps", type=int, default=50)
+    ap.add_argument("--profile-only", action="store_true",
+                    help="only the timed steps (for rocprofv3 runs)")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------------
+# synthetic data (device side)
+# ------------------------------------------------------------------------------------------------
+def make_centres(torch, cfg, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    cs = []
+    for d, c in zip(cfg["parts"], cfg["centres"]):
+        cs.append(torch.randn(c, d, generator=g).to(device) if c > 0 else None)
+    return cs
+
+
+def gen_block(torch, cfg, centres, b, device, seed, n=BLOCK):
+    g = torch.Generator(device=device).manual_seed(seed * 1_000_003 + b)
+    parts = []
+    for (d, c), cen in zip(zip(cfg["parts"], cfg["centres"]), centres):
+        if cen is None:
+            p = torch.randn(n, d, generator=g, device=device).abs_()
+        else:
+            idx = torch.randint(0, c, (n,), generator=g, device=device)
+            p = cen[idx] + 0.5 * torch.randn(n, d, generator=g, device=device)
+        p = p / p.norm(dim=1, keepdim=True).clamp_min(1e-30)
+        parts.append(p)
+    return torch.cat(parts, 1).contiguous()
+
+
+def gen_rows(torch, cfg, centres, r0, r1, device, seed):
+    """Rows [r0, r1) of the corpus, yielded in blocks (identical for any sharding)."""
+    b0, b1 = r0 // BLOCK, (r1 + BLOCK - 1) // BLOCK
+    for b in range(b0, b1):
+        blk = gen_block(torch, cfg, centres, b, device, seed)
+        lo, hi = max(r0, b * BLOCK) - b * BLOCK, min(r1, (b + 1) * BLOCK) - b * BLOCK
+        yield blk[lo:hi]
+
+
+def gen_queries(torch, cfg, centres, nq, device, seed):
+    q = gen_block(torch, cfg, centres, 10_000_000 + 7, device, seed + 17, n=nq)
+    return (q / q.norm(dim=1, keepdim=True)).contiguous()   # faiss.normalize_L2 after concat
+
+
+# ------------------------------------------------------------------------------------------------
+def exact_ground_truth(torch, dist, world, cfg, centres, r0, r1, q, k, device, seed):
+    """float64 exact top-k of this rank's shard, gathered and merged (recall reference)."""
+    qd = q.double()
+    qn = (qd * qd).sum(1, keepdim=True)
+    best_d = torch.full((q.shape[0], k), float("inf"), dtype=torch.float64, device=device)
+    best_i = torch.full((q.shape[0], k), -1, dtype=torch.int64, device=device)
+    pos = r0
+    for blk in gen_rows(torch, cfg, centres, r0, r1, device, seed):
+        xd = blk.double()
+        dd = qn + (xd * xd).sum(1)[None, :] - 2.0 * (qd @ xd.T)
+        kk = min(k, xd.shape[0])
+        v, i = torch.topk(dd, kk, dim=1, largest=False)
+        cat_d = torch.cat([best_d, v], 1)
+        cat_i = torch.cat([best_i, i + pos], 1)
+        v2, j = torch.topk(cat_d, k, dim=1, largest=False)
+        best_d, best_i = v2, torch.gather(cat_i, 1, j)
+        pos += xd.shape[0]
+    if world > 1:
+        gd = [torch.empty_like(best_d) for _ in range(world)]
+        gi = [torch.empty_like(best_i) for _ in range(world)]
+        dist.all_gather(gd, best_d)
+        dist.all_gather(gi, best_i)
+        cat_d, cat_i = torch.cat(gd, 1), torch.cat(gi, 1)
+        v2, j = torch.topk(cat_d, k, dim=1, largest=False)
+        best_d, best_i = v2, torch.gather(cat_i, 1, j)
+    return best_d.cpu().numpy(), best_i.cpu().numpy()
+
+
+def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
+    """Rank 0, N=1 only: the CPU comparator on a bounded sample of the same workload.
+
+    faiss-cpu (the reference's library, north_star's HNSW comparator) is not installed on this
+    image, so the comparator is the oracle's restatement of faiss IndexFlatL2's own BLAS search
+    (oracle.flat_knn.search_blas_fp32: sgemm + norms + partial sort, numpy's threaded BLAS).
+    Time scales linearly in corpus rows, so the sample's q/s is converted to the full corpus.
+    """
+    from oracle.flat_knn import search_blas_fp32
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()
+                     if p.get("user_api") == "blas"] or [os.cpu_count() or 1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    dev = "cuda"
+    rows = [blk.cpu().numpy() for blk in gen_rows(torch, cfg, centres, 0, 4 * BLOCK, dev, seed)]
+    xb = np.concatenate(rows)
+    xq = gen_queries(torch, cfg, centres, 256, dev, seed).cpu().numpy()
+    search_blas_fp32(xb[:4096], xq[:8], k)          # warm BLAS threads
+    t0 = time.perf_counter()
+    search_blas_fp32(xb, xq[:16], k)
+    t_probe = time.perf_counter() - t0
+    # choose (queries, reps) to fill about budget_s
+    per_query = t_probe / 16
+    nq = int(min(256, max(16, budget_s / 3 / max(per_query, 1e-9))))
+    times = []
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        search_blas_fp32(xb, xq[:nq], k)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_start > budget_s or len(times) >= 10:
+            break
+    t = float(np.median(times))
+    qps_sample = nq / t
+    qps_full = qps_sample * xb.shape[0] / D["rows"]
+    return {
+        "value": qps_full, "unit": "queries/s", "cores": int(cores), "kind": "port",
+        "sample": (f"{xb.shape[0]} rows x {xb.shape[1]} (first rows of the same corpus), "
+                   f"{nq} queries/batch, median of {len(times)} batches "
+                   f"({qps_sample:.1f} q/s on the sample, scaled x{xb.shape[0]}/{D['rows']} "
+                   f"rows); oracle.flat_knn.search_blas_fp32 = faiss exhaustive_L2sqr_blas "
+                   f"restated (faiss-cpu absent on the box)"),
+    }
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from image_recommender_amd import _lib
+    from image_recommender_amd.faiss_compat import METRIC_L2
+    from image_recommender_amd.sharded import ShardedIndex
+
+    cfg = dict(CONFIGS[a.config])
+    if a.rows:
+        cfg["rows"] = a.rows
+    D_total = int(sum(cfg["parts"]))
+    seed = a.config
+    centres = make_centres(torch, cfg, device, seed)
+    q = gen_queries(torch, cfg, centres, a.nq, device, seed)
+
+    shard = ShardedIndex(D_total, cfg["rows"], METRIC_L2, device=local)
+    t_build0 = time.perf_counter()
+    for blk in gen_rows(torch, cfg, centres, shard.row0, shard.row1, device, seed):
+        shard.add_local(blk)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_build0
+    lib = _lib.load()
+
+    def step():
+        return shard.search(q, a.k)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib.knn_set_timing(shard.index.handle, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        Dr, Ir = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    import ctypes as C
+    tot_ms, nl = C.c_double(), C.c_int()
+    _lib.check(lib.knn_kernel_time(shard.index.handle, C.byref(tot_ms), C.byref(nl)), "timing")
+    lib.knn_set_timing(shard.index.handle, 0)
+    el = torch.tensor([elapsed, tot_ms.value / max(nl.value, 1)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(el[0]), float(el[1])
+    if a.profile_only:
+        if rank == 0:
+            print(json.dumps({"elapsed_s": elapsed, "kernel_ms": kern_ms}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # recall@k on the first gt-queries queries, against float64 exact ground truth
+    ngt = min(a.gt_queries, a.nq)
+    gt_d, gt_i = exact_ground_truth(torch, dist, world, cfg, centres, shard.row0, shard.row1,
+                                    q[:ngt], a.k, device, seed)
+    got_i = Ir[:ngt].cpu().numpy()
+    got_d = Dr[:ngt].cpu().numpy()
+    hits = sum(len(set(x.tolist()) & set(y.tolist())) for x, y in zip(got_i, gt_i))
+    recall = hits / (a.k * ngt)
+    max_dist_err = float(np.max(np.abs(got_d.astype(np.float64) - gt_d)))
+
+    # single-query latency regime (the CLI's nq = 1 path; HBM-bound)
+    q1 = q[:1].contiguous()
+    for _ in range(3):
+        shard.search(q1, a.k)
+    torch.cuda.synchronize()
+    lib.knn_set_timing(shard.index.handle, 1)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(a.single_query_steps):
+        shard.search(q1, a.k)
+    torch.cuda.synchronize()
+    el1 = time.perf_counter() - t1
+    _lib.check(lib.knn_kernel_time(shard.index.handle, C.byref(tot_ms), C.byref(nl)), "timing")
+    lib.knn_set_timing(shard.index.handle, 0)
+    e1 = torch.tensor([el1, tot_ms.value / max(nl.value, 1)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(e1, op=dist.ReduceOp.MAX)
+    el1, kern1_ms = float(e1[0]), float(e1[1])
+
+    tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    lib.knn_plan(shard.index.handle, a.nq, a.k, C.byref(tr), C.byref(tq), C.byref(sp), C.byref(wg))
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(torch, cfg, centres, {"rows": cfg["rows"]}, a.k, seed, a.cpu_seconds)
+
+    if rank == 0:
+        n_local = shard.local_rows
+        flops = 2.0 * n_local * D_total * a.nq
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        bytes1 = 4.0 * n_local * D_total + 4.0 * n_local
+        qps = a.nq * a.steps / elapsed
+        out = {
+            "metric": "k-NN queries/sec + recall@10 on 1M concat vectors at 1/2/4/8 MI355X",
+            "value": qps,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic, generated on device (Gaussian-mixture parts, per-part L2-normalised)",
+            "config": {
+                "workload": cfg["name"], "rows": cfg["rows"], "dim": D_total, "k": a.k,
+                "queries_per_batch": a.nq, "metric": "L2 on normalised queries (cosine ranking)",
+                "rows_per_gpu": n_local, "parallelism": f"row-shard x{world} + RCCL all-gather merge",
+                "tile_rows": tr.value, "tile_queries": tq.value, "row_splits": sp.value,
+                "workgroups": wg.value,
+            },
+            "recall_at_10": recall,
+            "recall_queries": ngt,
+            "max_abs_dist_err_vs_fp64": max_dist_err,
+            "roofline": {
+                "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS, "traffic": None,
+                "kernel": "knn_tile_topk_kernel<1,8,16>", "kernel_ms": kern_ms,
+                "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
+            },
+            "single_query": {
+                "queries_per_s": a.single_query_steps / el1,
+                "kernel_ms": kern1_ms,
+                "hbm_gbs": bytes1 / (kern1_ms * 1e-3) / 1e9,
+                "hbm_frac": bytes1 / (kern1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            },
+            "build_s": build_s,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

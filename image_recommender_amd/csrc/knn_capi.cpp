@@ -157,7 +157,12 @@ int reserve_rows(knn_index* ix, int64_t need) {
     return KNN_OK;
 }
 
-hipStream_t pick(knn_index* ix, void* s) { return s ? (hipStream_t)s : ix->stream; }
+// *_device entry points run on the caller's stream; NULL is the HIP null (default) stream, as in
+// every HIP API (torch's default stream has handle 0).
+hipStream_t pick(knn_index* ix, void* s) {
+    (void)ix;
+    return (hipStream_t)s;
+}
 
 int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                   hipStream_t st) {

@@ -1,0 +1,103 @@
+"""Row-sharded exact k-NN over one node's GPUs.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  The corpus is split
+into contiguous row ranges, rank r owning global labels [r*N/G, (r+1)*N/G) — the offsets table of
+the reference (main/create_index.py:236-249) is unchanged by sharding.  A search runs the fused
+kernel on every shard (labels already global via knn_set_id_offset), all-gathers the per-shard
+(nq, k) results (nq*k*12 bytes per rank: latency-bound, far below one xGMI link) and merges the
+G*k candidates per query with the same (key, label) order as a single-GPU search, so sharded and
+unsharded results are identical.
+
+The reference has no multi-device code at all; this module replaces nothing but extends
+``index.search`` (main/search_from_image.py:247) to corpora larger than one GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .faiss_compat import METRIC_L2, Index, _METRIC_TO_KNN
+
+
+def shard_range(ntotal: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous balanced row range of `rank` (same formula as the kernel's row splits)."""
+    return ntotal * rank // world, ntotal * (rank + 1) // world
+
+
+def gather_results(D, I, group=None):
+    """All-gather per-rank (nq, k) results into (world, nq, k) tensors on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if world == 1:
+        return D.unsqueeze(0), I.unsqueeze(0)
+    gD = torch.empty((world,) + tuple(D.shape), dtype=D.dtype, device=D.device)
+    gI = torch.empty((world,) + tuple(I.shape), dtype=I.dtype, device=I.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(gD, D.contiguous(), group=group)
+        dist.all_gather_into_tensor(gI, I.contiguous(), group=group)
+    else:   # gloo (CPU tests): list form
+        dist.all_gather(list(gD.unbind(0)), D.contiguous(), group=group)
+        dist.all_gather(list(gI.unbind(0)), I.contiguous(), group=group)
+    return gD, gI
+
+
+def merge_gathered_device(gD, gI, k: int, metric: int = METRIC_L2, stream: int = 0):
+    """HIP merge of gathered (world, nq, kin) device results into the final (nq, k)."""
+    import torch
+    world, nq, kin = gD.shape
+    D = torch.empty((nq, k), dtype=torch.float32, device=gD.device)
+    I = torch.empty((nq, k), dtype=torch.int64, device=gD.device)
+    _lib.check(_lib.load().knn_merge_device(
+        C.c_void_p(gD.data_ptr()), C.c_void_p(gI.data_ptr()), int(world), int(nq), int(kin),
+        int(k), _METRIC_TO_KNN[metric], C.c_void_p(D.data_ptr()), C.c_void_p(I.data_ptr()),
+        C.c_void_p(stream or None)), "knn_merge_device")
+    return D, I
+
+
+class ShardedIndex:
+    """This rank's shard of a row-partitioned exact index, plus the collective search."""
+
+    def __init__(self, d: int, ntotal_global: int, metric: int = METRIC_L2, group=None,
+                 device: int | None = None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.d, self.metric, self.ntotal_global = int(d), metric, int(ntotal_global)
+        self.row0, self.row1 = shard_range(self.ntotal_global, self.rank, self.world)
+        dev = torch.cuda.current_device() if device is None else device
+        self.device = dev
+        self.index = Index(d, metric, dev)
+        self.index.set_id_offset(self.row0)
+        self.index.reserve(self.row1 - self.row0)
+
+    @property
+    def local_rows(self) -> int:
+        return self.row1 - self.row0
+
+    def add_local(self, x) -> None:
+        """Append rows of this shard (torch device tensor or host array, in global order)."""
+        import torch
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            x = x.contiguous()
+            self.index.add_device(x.data_ptr(), x.shape[0],
+                                  torch.cuda.current_stream(x.device).cuda_stream)
+        else:
+            self.index.add(np.asarray(x, dtype=np.float32))
+
+    def search(self, q, k: int):
+        """q: (nq, d) float32 device tensor, identical on every rank -> (D, I) on every rank."""
+        import torch
+        nq = q.shape[0]
+        st = torch.cuda.current_stream(q.device).cuda_stream
+        D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+        I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+        self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
+        if self.world == 1:
+            return D, I
+        gD, gI = gather_results(D, I, self.group)
+        return merge_gathered_device(gD, gI, k, self.metric, st)

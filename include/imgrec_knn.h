@@ -23,7 +23,7 @@
  *     last failure on the calling thread is returned by knn_last_error().
  *   - Host-pointer functions (knn_add, knn_search, knn_write, ...) synchronise before returning.
  *     *_device functions take device pointers and a hipStream_t (passed as void*; NULL = the
- *     index's own stream), enqueue asynchronously and never synchronise or allocate when the
+ *     HIP null stream, like any HIP API), enqueue asynchronously and never synchronise or allocate when the
  *     workspace is already large enough (so a caller may capture them into a hipGraph).
  *   - Vectors are row-major float32, n rows × d.  Labels are int64.  Result rows are sorted by
  *     ascending distance (L2) or descending inner product (IP/COSINE); exact ties are broken by the

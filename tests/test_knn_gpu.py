@@ -169,3 +169,28 @@ def test_search_larger_batch_chunks(faiss):
     D, I = idx.search(xq, 4)
     sel = np.r_[0:40, 8180:8200, 8990:9000]
     check_knn(D[sel], I[sel], xb, xq[sel], 4, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("n,d,nq", [(100_000, 256, 300), (400_000, 64, 5), (150_000, 128, 100)])
+def test_many_row_tiles_per_workgroup(faiss, n, d, nq):
+    """Corpora large enough that every workgroup walks several row tiles (the bench regime)."""
+    xb = mixture(n, d, centres=200, seed=n % 97)
+    xq = mixture(nq, d, centres=200, seed=n % 89)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    D, I = idx.search(xq, 10)
+    sel = np.arange(min(nq, 24))
+    check_knn(D[sel], I[sel], xb, xq[sel], 10, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("d", [48, 1968])
+def test_many_row_tiles_odd_depth_steps(faiss, d):
+    """Odd number of 16-deep stages (48 -> 3, 1968 -> 123) with several tiles per workgroup."""
+    n = 120_000 if d == 48 else 60_000
+    xb = concat_rows(n, seed=5) if d == 1968 else mixture(n, d, centres=100, seed=9)
+    xq = xb[:300].copy() + 0.01
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    D, I = idx.search(xq, 10)
+    sel = np.arange(16)
+    check_knn(D[sel], I[sel], xb, xq[sel], 10, "l2", min_exact_frac=0.5)
