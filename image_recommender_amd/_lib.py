@@ -11,7 +11,7 @@ import os
 import threading
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libimgrec.so"
+LIB_PATH = Path(__file__).resolve().parent / "lib" / os.environ.get("IMGREC_LIB_NAME", "libimgrec.so")
 
 # Error codes of include/imgrec_knn.h
 KNN_OK, KNN_EINVAL, KNN_EHIP, KNN_ENOMEM, KNN_EIO, KNN_ENOSYS = 0, -1, -2, -3, -4, -5

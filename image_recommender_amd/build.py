@@ -23,8 +23,9 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIBDIR = PKG / "lib"
-OBJDIR = PKG.parent / "build" / "obj"
-LIB = LIBDIR / "libimgrec.so"
+OBJDIR = PKG.parent / "build" / ("obj" + os.environ.get("IMGREC_OBJ_SUFFIX", ""))
+LIB = LIBDIR / os.environ.get("IMGREC_LIB_NAME", "libimgrec.so")
+EXTRA_FLAGS = os.environ.get("IMGREC_EXTRA_FLAGS", "").split()
 ARCH = os.environ.get("IMGREC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["knn_kernels.hip", "knn_capi.cpp", "color_hist.hip", "ingest.cpp"]
@@ -51,7 +52,7 @@ def _compile(src: Path, obj: Path, force: bool) -> str:
     if not force and not _stale(obj, deps):
         return f"up to date: {obj.name}"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-           "-Wno-unused-function", "-c", str(src), "-o", str(obj)]
+           "-Wno-unused-function", *EXTRA_FLAGS, "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -81,7 +81,7 @@ struct Plan {
 // Fused-kernel geometry for one query chunk (see DESIGN.md "Launch plan").
 Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
     Plan p{};
-    p.km = k <= 8 ? 8 : (k <= 16 ? 16 : 32);
+    p.km = k <= 8 ? 8 : (k <= 10 ? 10 : (k <= 16 ? 16 : 32));
     int wg_per_cu;
     if (nq <= 32) { p.wr = 2; p.wq = 1; wg_per_cu = 3; }
     else if (nq <= 128) { p.wr = 2; p.wq = 2; wg_per_cu = 2; }

@@ -101,33 +101,106 @@ rows_ingest_kernel(const float* __restrict__ src, int64_t n, int d, int dp, int6
 
 // ---------------------------------------------------------------------------------------------
 // knn_tile_topk
+//
+// Workgroup = WR x WQ waves; wave tile = 128 corpus rows (4 MFMA row blocks) x 32 queries, so the
+// workgroup tile is BM = 128*WR rows x BQ = 32*WQ queries.  A workgroup owns one query block and a
+// contiguous range of row tiles (a "row split") and streams it as one continuous sequence of
+// 16-deep K stages: (tile t0, stage 0..nsteps-1), (t0+1, 0..), ...
+//
+// Staging is LDS-DMA (global_load_lds_dwordx4): each wave instruction moves one 1-KiB piece =
+// 16 rows x 64 B straight into LDS (no staging VGPRs), into an NS-deep ring; a stage is read NS-1
+// iterations after its loads were issued, behind a counted `s_waitcnt vmcnt` and one raw
+// s_barrier per stage (cdna_hip_programming.md §5 "Pipelining across barriers").  The ring runs
+// across tile boundaries, so the top-k epilogue of a tile overlaps the next tile's loads.
+//
+// LDS image: rows of 16 floats (64 B), 16-B chunk c of row r stored at chunk c ^ ((r >> 2) & 3).
+// The XOR is applied to the per-lane GLOBAL source address (the DMA destination is lane-linear);
+// the fragment reads apply the same XOR, which makes every ds_read_b128 16-lane group hit 16
+// distinct 16-B bank slots.
 // ---------------------------------------------------------------------------------------------
-constexpr int BK = 16;     // depth of one LDS stage
-constexpr int LROW = 20;   // floats per staged row: 16 + 4 pad -> 80-B stride, conflict-free b128
+constexpr int BK = 16;     // depth of one stage (floats)
 
-template <int WR, int WQ, int KM>
+template <int WR, int WQ, int NS>
+struct TileGeom {
+    static constexpr int NW = WR * WQ, NT = NW * 64;
+    static constexpr int BM = WR * 128, BQ = WQ * 32;
+    static constexpr int SA = BM * BK, SB = BQ * BK, STAGE = SA + SB;   // floats
+    static constexpr int PA = BM / 16, PB = BQ / 16, PIECES = PA + PB;  // 1-KiB pieces / stage
+    static constexpr int LPW = PIECES / NW;                            // pieces per wave
+    static constexpr int PARK = NW * 16 * 64;                          // epilogue key parking
+    static constexpr int LDS_FLOATS = NS * STAGE + PARK + NS * BM;
+    static_assert(PIECES % NW == 0, "pieces must divide evenly over waves");
+    static_assert(BM % 64 == 0, "norm DMA uses whole waves");
+};
+
+// LDS byte address of a pointer into __shared__ memory.
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)p);
+}
+
+// LDS-DMA issued from inline asm (M0 = wave-uniform LDS destination, set and restored inside the
+// statement).  hipcc does not see these as LDS writes, so it inserts no vmcnt(0) in front of the
+// fragment ds_reads (it would for __builtin_amdgcn_global_load_lds, serialising the ring); every
+// wait on them is the explicit counted wait_vmcnt below.
+__device__ __forceinline__ void dma16(const float* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma4(const float* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+// s_barrier that also orders the compiler's LDS accesses (the intrinsic alone is IntrNoMem).
+__device__ __forceinline__ void barrier_raw() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Insert into an ascending list when labels reach this lane in increasing order (true inside
+// the fused kernel: a lane visits its rows in increasing row order), so "ranks before" is a plain
+// key comparison and an equal key always lands behind the existing entries.
+template <int K>
+__device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], float d, int id) {
+#pragma unroll
+    for (int p = K - 1; p > 0; --p) {
+        const bool shift = d < kd[p - 1];
+        const bool here = !shift && d < kd[p];
+        kd[p] = shift ? kd[p - 1] : (here ? d : kd[p]);
+        ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
+    }
+    const bool here0 = d < kd[0];
+    kd[0] = here0 ? d : kd[0];
+    ki[0] = here0 ? id : ki[0];
+}
+
+template <int WR, int WQ, int KM, int NS>
 __global__ void __launch_bounds__(WR * WQ * 64)
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
                      int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
                      int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
                      float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand) {
-    constexpr int NT = WR * WQ * 64;
-    constexpr int BM = WR * 128;   // corpus rows per tile (wave tile: 128 rows = 4 row blocks)
-    constexpr int BQ = WQ * 32;    // queries per tile   (wave tile: 32 queries)
-    constexpr int A4 = BM * 4;     // float4 per A stage (BM rows x 16 floats)
-    constexpr int B4 = BQ * 4;
-    constexpr int AP = (A4 + NT - 1) / NT;
-    constexpr int BP = (B4 + NT - 1) / NT;
+    using G = TileGeom<WR, WQ, NS>;
+    constexpr int NW = G::NW, BM = G::BM, BQ = G::BQ, SA = G::SA, STAGE = G::STAGE;
+    constexpr int PA = G::PA, LPW = G::LPW;
 
-    // One LDS allocation: [A stage 0 | A stage 1 | B stage 0 | B stage 1 | row norms].  The
-    // stage region doubles as the epilogue's per-wave key parking (16 x 64 floats per wave).
-    constexpr int SA = BM * LROW, SB = BQ * LROW;
-    static_assert(2 * (SA + SB) >= WR * WQ * 16 * 64, "parking area exceeds stage buffers");
-    __shared__ __attribute__((aligned(16))) float smem[2 * SA + 2 * SB + BM];
-    float* const Ns = smem + 2 * SA + 2 * SB;
+    __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
+    float* const park_base = smem + NS * STAGE;
+    float* const norm_base = park_base + G::PARK;
 
     // XCD-aware, bijective block -> (query block, row split) map: blocks b and b+8 share an XCD;
-    // consecutive remapped ids (same XCD) share a row split so the corpus tile they stream is
+    // consecutive remapped ids (same XCD) share a row split, so the corpus stages they stream are
     // served from that XCD's L2 for all query blocks.
     const int nwg = gridDim.x, wg = blockIdx.x;
     const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -139,14 +212,22 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave / WQ;
     const int wq = wave % WQ;
     const int li = lane & 31;
     const int lh = lane >> 5;
     const int qcol = qb * BQ + wq * 32 + li;     // the query this lane owns (< nq_pad)
     const bool qvalid = qcol < nq;
-    const float qn = (metric == 1) ? qnorm[qcol] : 0.f;
+    float qn = (metric == 1) ? qnorm[qcol] : 0.f;
+    asm volatile("" : "+v"(qn));   // consume the load here, before the DMA stream starts
+
+    // per-lane DMA source offset inside a piece: row (lane >> 2), logical chunk swizzled
+    const int goff = (lane >> 2) * dp + 4 * ((lane & 3) ^ ((lane >> 4) & 3));
+    // per-lane fragment offsets inside a 32-row block: logical chunks 2h, 2h+1 of row li
+    const int sw = (li >> 2) & 3;
+    const int fo0 = li * BK + 4 * ((2 * lh) ^ sw);
+    const int fo1 = li * BK + 4 * ((2 * lh + 1) ^ sw);
 
     float kd[KM];
     int ki[KM];
@@ -156,67 +237,71 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     const int nsteps = dp / BK;
     const float* qbase = qp + (size_t)qb * BQ * dp;
 
+    // ---- DMA issue cursor (runs NS-1 stages ahead of the consumer) -------------------------
+    int it = t0, is = 0, ibuf = 0;
+    auto issue_next = [&]() __attribute__((always_inline)) {
+        if (it >= t1) return;
+        const uint32_t st = lds_addr(smem) + (uint32_t)(ibuf * STAGE) * 4u;
+        if (is == 0) {                      // row norms of the tile, one 4-B DMA per lane
+            for (int j = wave; j < BM / 64; j += NW)
+                dma4(xnorm + (size_t)it * BM + j * 64 + lane,
+                     lds_addr(norm_base) + (uint32_t)(((it - t0) % NS) * BM + j * 64) * 4u);
+        }
+        const int k0 = is * BK;
+#pragma unroll
+        for (int j = 0; j < LPW; ++j) {
+            const int pc = wave * LPW + j;      // wave-uniform
+            const float* src;
+            uint32_t dst;
+            if (pc < PA) {
+                src = xb + ((size_t)it * BM + pc * 16) * dp + k0 + goff;
+                dst = st + (uint32_t)(pc * 256) * 4u;
+            } else {
+                src = qbase + (size_t)(pc - PA) * 16 * dp + k0 + goff;
+                dst = st + (uint32_t)(SA + (pc - PA) * 256) * 4u;
+            }
+            dma16(src, dst);
+        }
+        if (++is == nsteps) { is = 0; ++it; }
+        ibuf = (ibuf + 1 == NS) ? 0 : ibuf + 1;
+    };
+
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j) issue_next();
+    const int64_t total = (int64_t)(t1 - t0) * nsteps;
+    int64_t g = 0;
+    int cbuf = 0;
+
     for (int t = t0; t < t1; ++t) {
         const int row0 = t * BM;
-        const float* abase = xb + (size_t)row0 * dp;
-
         f32x16 acc[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[b] = (f32x16){0.f};
 
-        float4 ra[AP], rb[BP];
-        auto load_stage = [&](int k0) {
-#pragma unroll
-            for (int p = 0; p < AP; ++p) {
-                const int f = tid + p * NT;
-                if (A4 % NT == 0 || f < A4)
-                    ra[p] = *reinterpret_cast<const float4*>(abase + (size_t)(f >> 2) * dp + k0 + (f & 3) * 4);
-            }
-#pragma unroll
-            for (int p = 0; p < BP; ++p) {
-                const int f = tid + p * NT;
-                if (B4 % NT == 0 || f < B4)
-                    rb[p] = *reinterpret_cast<const float4*>(qbase + (size_t)(f >> 2) * dp + k0 + (f & 3) * 4);
-            }
-        };
-        auto store_stage = [&](int buf) {
-#pragma unroll
-            for (int p = 0; p < AP; ++p) {
-                const int f = tid + p * NT;
-                if (A4 % NT == 0 || f < A4)
-                    *reinterpret_cast<float4*>(&smem[buf * SA + (f >> 2) * LROW + (f & 3) * 4]) = ra[p];
-            }
-#pragma unroll
-            for (int p = 0; p < BP; ++p) {
-                const int f = tid + p * NT;
-                if (B4 % NT == 0 || f < B4)
-                    *reinterpret_cast<float4*>(&smem[2 * SA + buf * SB + (f >> 2) * LROW + (f & 3) * 4]) = rb[p];
-            }
-        };
+        for (int s = 0; s < nsteps; ++s, ++g) {
+            // own DMA of stage g landed (loads of the stages issued after it may stay in flight)
+            const int64_t ahead = total - 1 - g;     // stages after g that have been issued
+            if (ahead >= NS - 2) wait_vmcnt<LPW * (NS - 2)>();
+            else if (NS > 3 && ahead == 1) wait_vmcnt<LPW>();
+            else wait_vmcnt<0>();
+            barrier_raw();                           // everyone's DMA landed; stage g-1 fully read
+            issue_next();                            // refills the buffer stage g-1 used
 
-        load_stage(0);
-        for (int r = tid; r < BM; r += NT) Ns[r] = xnorm[row0 + r];
-        store_stage(0);
-        __syncthreads();
-
-        int cur = 0;
-        for (int s = 0; s < nsteps; ++s) {
-            const bool more = (s + 1) < nsteps;
-            if (more) load_stage((s + 1) * BK);
-
+            const float* st = smem + cbuf * STAGE;
+            cbuf = (cbuf + 1 == NS) ? 0 : cbuf + 1;
             float a[4][8], bq[8];
             {
-                const float* bp = &smem[2 * SA + cur * SB + (wq * 32 + li) * LROW + lh * 8];
-                const float4 b0 = *reinterpret_cast<const float4*>(bp);
-                const float4 b1 = *reinterpret_cast<const float4*>(bp + 4);
+                const float* bp = st + SA + wq * 32 * BK;
+                const float4 b0 = *reinterpret_cast<const float4*>(bp + fo0);
+                const float4 b1 = *reinterpret_cast<const float4*>(bp + fo1);
                 bq[0] = b0.x; bq[1] = b0.y; bq[2] = b0.z; bq[3] = b0.w;
                 bq[4] = b1.x; bq[5] = b1.y; bq[6] = b1.z; bq[7] = b1.w;
             }
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const float* ap = &smem[cur * SA + (wr * 128 + b * 32 + li) * LROW + lh * 8];
-                const float4 a0 = *reinterpret_cast<const float4*>(ap);
-                const float4 a1 = *reinterpret_cast<const float4*>(ap + 4);
+                const float* ap = st + (wr * 128 + b * 32) * BK;
+                const float4 a0 = *reinterpret_cast<const float4*>(ap + fo0);
+                const float4 a1 = *reinterpret_cast<const float4*>(ap + fo1);
                 a[b][0] = a0.x; a[b][1] = a0.y; a[b][2] = a0.z; a[b][3] = a0.w;
                 a[b][4] = a1.x; a[b][5] = a1.y; a[b][6] = a1.z; a[b][7] = a1.w;
             }
@@ -226,37 +311,38 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                 for (int b = 0; b < 4; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
             }
-
-            if (more) store_stage(cur ^ 1);
-            __syncthreads();
-            cur ^= 1;
         }
 
-        // Epilogue: key = L2 distance (faiss exhaustive_L2sqr_blas form, clamped at 0) or -ip.
-        // Keys of one 32x32 block are screened against the lane's current K-th key; only when a
-        // lane of the wave has a survivor are the 16 keys parked in (now idle) stage LDS and
-        // inserted one by one, so the list insert is emitted once per block, not per register.
+        // ---- epilogue: key = L2 distance (faiss exhaustive_L2sqr_blas form, clamped at 0) or
+        // -ip; screened against this lane's K-th key and (<=) its partner lane's K-th key (the
+        // partner holds the same query's other rows: a key worse than the partner's K-th cannot
+        // reach the union's top K).  Survivors are parked in per-wave LDS and inserted one by one.
+#ifdef IMGREC_ABLATE_NO_EPILOGUE
+        if (qvalid && row0 < 0) {   // never taken: keeps the accumulators live, no top-k work
+#else
         if (qvalid) {
-            float* park = smem + wave * (16 * 64);
+#endif
+            const float* nrm = norm_base + ((t - t0) % NS) * BM;
+            float* park = park_base + wave * (16 * 64);
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 float key[16];
                 unsigned mask = 0;
-                const float tau_d = kd[KM - 1];
-                const int tau_i = ki[KM - 1];
+                const float tau = kd[KM - 1];
+                const float tau_p = __shfl_xor(tau, 32, 64);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
                     const int rl = wr * 128 + b * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
                     const float ip = acc[b][r];
                     float kv;
                     if (metric == 1) {
-                        kv = fmaf(-2.f, ip, qn + Ns[rl]);
+                        kv = fmaf(-2.f, ip, qn + nrm[rl]);
                         kv = kv < 0.f ? 0.f : kv;
                     } else {
                         kv = -ip;
                     }
                     key[r] = kv;
-                    const bool pass = (row0 + rl < nrows) && ranks_before(kv, row0 + rl, tau_d, tau_i);
+                    const bool pass = (row0 + rl < nrows) && kv < tau && kv <= tau_p;
                     mask |= (unsigned)pass << r;
                 }
                 if (__any(mask != 0)) {
@@ -267,14 +353,12 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                         if ((mask >> r) & 1u) {
                             const float kv = park[r * 64 + lane];
                             const int row = row0 + wr * 128 + b * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                            if (ranks_before(kv, row, kd[KM - 1], ki[KM - 1]))
-                                list_insert<KM, int>(kd, ki, kv, row);
+                            if (kv < kd[KM - 1]) list_insert_mono<KM>(kd, ki, kv, row);
                         }
                     }
                 }
             }
         }
-        __syncthreads();   // Ns / stage buffers are rewritten by the next tile's prologue
     }
 
     if (qvalid) {
@@ -363,15 +447,16 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
     return hipGetLastError();
 }
 
-template <int WR, int WQ>
+template <int WR, int WQ, int NS>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
-    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV>), grid, block, 0, st, a.xb, a.xnorm,     \
-                       a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, a.nqb,    \
-                       a.id_offset, a.cand_d, a.cand_i, a.ncand)
+    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS>), grid, block, 0, st, a.xb,         \
+                       a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
+                       a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
     switch (km) {
         case 8: IMGREC_LAUNCH_TILE(8); break;
+        case 10: IMGREC_LAUNCH_TILE(10); break;
         case 16: IMGREC_LAUNCH_TILE(16); break;
         case 32: IMGREC_LAUNCH_TILE(32); break;
         default: return hipErrorInvalidValue;
@@ -381,9 +466,9 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
-    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8>(a.km, a, st);
-    if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2>(a.km, a, st);
-    if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1>(a.km, a, st);
+    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, 4>(a.km, a, st);
+    if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2, 3>(a.km, a, st);
+    if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1, 3>(a.km, a, st);
     return hipErrorInvalidValue;
 }
 

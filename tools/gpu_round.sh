@@ -1,0 +1,13 @@
+#!/bin/bash
+# tests + bench + kernel-stats profile; every GPU step under its own timeout, stop at first failure
+set -u
+export PYTHONPATH=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
+TAG=${1:-run}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 2; }
+cat $OUT/bench.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; exit 3; }
+head -6 $OUT/prof/run_kernel_stats.csv | cut -c1-200
