@@ -372,33 +372,20 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 }
 
 // ---------------------------------------------------------------------------------------------
-// knn_merge: one wave per query.  Candidate (q, l, p) lives at q*stride_q + l*stride_l + p.
+// knn_merge: WPQ waves per query.  The input is nlists candidate lists per query, each sorted
+// best-first (the fused kernel's per-lane lists, or gathered per-shard results); list l of query q
+// starts at q*stride_q + l*stride_l and holds kin entries, label -1 marking an empty tail.
+// A lane walks whole lists with 8-wide batches of independent loads and stops at the first entry
+// that does not beat its running K-th (everything after it in a sorted list is worse); the lanes'
+// lists are then reduced by k rounds of a 64-lane (key, label) argmin, per wave and, for WPQ > 1,
+// once more over the waves' results through LDS.
 // ---------------------------------------------------------------------------------------------
+// k rounds of a wave-wide (key, label) argmin over the lanes' sorted lists.  Lane 0 writes round
+// r to out_d/out_i[r] (memory, never a private array: a runtime index would go to scratch); with
+// final != 0 it writes the faiss output convention (IP sign restored, empty = -1 / +-FLT_MAX).
 template <int KM>
-__global__ void __launch_bounds__(256)
-knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
-                 int nlists, int kin, int64_t stride_q, int64_t stride_l, int k, int metric,
-                 int negate_in, float* __restrict__ D, int64_t* __restrict__ I) {
-    const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
-
-    float kd[KM];
-    int64_t ki[KM];
-#pragma unroll
-    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
-
-    const int total = nlists * kin;
-    for (int c = lane; c < total; c += 64) {
-        const int l = c / kin, p = c - l * kin;
-        const int64_t off = q * stride_q + (int64_t)l * stride_l + p;
-        const int64_t id = ci[off];
-        if (id < 0) continue;
-        // gathered search results carry output-convention values (IP: larger first): re-key
-        const float d = negate_in ? -cd[off] : cd[off];
-        if (ranks_before(d, id, kd[KM - 1], ki[KM - 1])) list_insert<KM, int64_t>(kd, ki, d, id);
-    }
-
+__device__ __forceinline__ void wave_select(float (&kd)[KM], int64_t (&ki)[KM], int k, int lane,
+                                            float* out_d, int64_t* out_i, int final, int metric) {
     for (int r = 0; r < k; ++r) {
         float bd = kd[0];
         int64_t bi = ki[0];
@@ -420,13 +407,80 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
             ki[KM - 1] = -1;
         }
         if (lane == 0) {
-            float out;
-            if (bi < 0) out = (metric == 1) ? FLT_MAX : -FLT_MAX;
-            else out = (metric == 1) ? bd : -bd;
-            D[q * k + r] = out;
-            I[q * k + r] = bi;
+            if (final) {
+                out_d[r] = bi < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX) : ((metric == 1) ? bd : -bd);
+            } else {
+                out_d[r] = bi < 0 ? INFINITY : bd;
+            }
+            out_i[r] = bi;
         }
     }
+}
+
+template <int KM, int WPQ>
+__global__ void __launch_bounds__(256)
+knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
+                 int nlists, int kin, int64_t stride_q, int64_t stride_l, int k, int metric,
+                 int negate_in, float* __restrict__ D, int64_t* __restrict__ I) {
+    constexpr int QPB = 4 / WPQ;                     // queries per 256-thread block
+    __shared__ float sd[4][KM];
+    __shared__ int64_t si[4][KM];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int64_t q = (int64_t)blockIdx.x * QPB + wave / WPQ;
+    const int sub = wave % WPQ;
+    const bool active = q < nq;
+
+    float kd[KM];
+    int64_t ki[KM];
+#pragma unroll
+    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+
+    if (active) {
+        for (int l = sub * 64 + lane; l < nlists; l += 64 * WPQ) {
+            const float* lp = cd + q * stride_q + (int64_t)l * stride_l;
+            const int64_t* ip = ci + q * stride_q + (int64_t)l * stride_l;
+            bool stop = false;
+            for (int p0 = 0; p0 < kin && !stop; p0 += 8) {
+                float d8[8];
+                int64_t i8[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {         // clamped index: loads are unconditional
+                    const int p = min(p0 + j, kin - 1);
+                    d8[j] = lp[p];
+                    i8[j] = ip[p];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float d = negate_in ? -d8[j] : d8[j];
+                    const bool ok = !stop && (p0 + j < kin) && i8[j] >= 0 &&
+                                    ranks_before(d, i8[j], kd[KM - 1], ki[KM - 1]);
+                    stop = stop || !ok;
+                    if (ok) list_insert<KM, int64_t>(kd, ki, d, i8[j]);
+                }
+            }
+        }
+    }
+
+    if (WPQ == 1) {
+        if (active) wave_select<KM>(kd, ki, k, lane, D + q * k, I + q * k, 1, metric);
+        return;
+    }
+    // WPQ == 4: one query per block; every wave's top-k to LDS, wave 0 merges the 4k.
+    wave_select<KM>(kd, ki, k, lane, sd[wave], si[wave], 0, metric);
+    __syncthreads();
+    if (wave != 0 || !active) return;
+#pragma unroll
+    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+    if (lane < 4) {
+        for (int r = 0; r < k; ++r) {
+            const float d = sd[lane][r];
+            const int64_t id = si[lane][r];
+            if (id < 0) break;
+            list_insert<KM, int64_t>(kd, ki, d, id);
+        }
+    }
+    wave_select<KM>(kd, ki, k, lane, D + q * k, I + q * k, 1, metric);
 }
 
 __global__ void fill_empty_kernel(float* __restrict__ D, int64_t* __restrict__ I, int64_t n,
@@ -476,18 +530,25 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
-    const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
-    if (k <= 8)
-        hipLaunchKernelGGL(knn_merge_kernel<8>, grid, block, 0, st, cd, ci, nq, nlists, kin, stride_q,
-                           stride_l, k, metric, negate_in, D, I);
-    else if (k <= 16)
-        hipLaunchKernelGGL(knn_merge_kernel<16>, grid, block, 0, st, cd, ci, nq, nlists, kin,
-                           stride_q, stride_l, k, metric, negate_in, D, I);
-    else if (k <= 32)
-        hipLaunchKernelGGL(knn_merge_kernel<32>, grid, block, 0, st, cd, ci, nq, nlists, kin,
-                           stride_q, stride_l, k, metric, negate_in, D, I);
-    else
-        return hipErrorInvalidValue;
+    // few queries with many lists: 4 waves per query; otherwise one wave per query
+    const bool wide = nq < 1024 && nlists > 256;
+    const dim3 block(256);
+    const dim3 grid((unsigned)(wide ? nq : (nq + 3) / 4));
+#define IMGREC_LAUNCH_MERGE(KMV)                                                                    \
+    do {                                                                                            \
+        if (wide)                                                                                   \
+            hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, nq, nlists, \
+                               kin, stride_q, stride_l, k, metric, negate_in, D, I);               \
+        else                                                                                        \
+            hipLaunchKernelGGL((knn_merge_kernel<KMV, 1>), grid, block, 0, st, cd, ci, nq, nlists, \
+                               kin, stride_q, stride_l, k, metric, negate_in, D, I);               \
+    } while (0)
+    if (k <= 8) IMGREC_LAUNCH_MERGE(8);
+    else if (k <= 10) IMGREC_LAUNCH_MERGE(10);
+    else if (k <= 16) IMGREC_LAUNCH_MERGE(16);
+    else if (k <= 32) IMGREC_LAUNCH_MERGE(32);
+    else return hipErrorInvalidValue;
+#undef IMGREC_LAUNCH_MERGE
     return hipGetLastError();
 }
 

@@ -194,3 +194,52 @@ def test_many_row_tiles_odd_depth_steps(faiss, d):
     D, I = idx.search(xq, 10)
     sel = np.arange(16)
     check_knn(D[sel], I[sel], xb, xq[sel], 10, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+@pytest.mark.parametrize("shards,nq,k", [(2, 7, 10), (4, 300, 5), (8, 1, 10), (3, 1100, 16)])
+def test_sharded_merge_is_bit_identical(faiss, metric, shards, nq, k):
+    """Row shards with global id offsets + the all-gather layout merge (knn_merge_device) give
+    exactly the single-index result: same distances, same labels."""
+    import torch
+    from image_recommender_amd.sharded import merge_gathered_device, shard_range
+    n, d = 20000, 160
+    xb = mixture(n, d, centres=80, seed=shards * 7 + nq)
+    xq = mixture(nq, d, centres=80, seed=nq + 1)
+    M = faiss.METRIC_L2 if metric == "l2" else faiss.METRIC_INNER_PRODUCT
+    full = faiss.IndexFlat(d, M)
+    full.add(xb)
+    Df, If = full.search(xq, k)
+    gD = torch.empty((shards, nq, k), dtype=torch.float32, device="cuda")
+    gI = torch.empty((shards, nq, k), dtype=torch.int64, device="cuda")
+    q = torch.from_numpy(xq).cuda()
+    for r in range(shards):
+        r0, r1 = shard_range(n, r, shards)
+        sh = faiss.IndexFlat(d, M)
+        sh.set_id_offset(r0)
+        sh.add(xb[r0:r1])
+        sh.search_device(q.data_ptr(), nq, k, gD[r].data_ptr(), gI[r].data_ptr(), 0)
+    D, I = merge_gathered_device(gD, gI, k, M)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(I.cpu().numpy(), If)
+    np.testing.assert_array_equal(D.cpu().numpy(), Df)
+
+
+def test_merge_device_padding_and_partial_lists(faiss):
+    """Shards smaller than k: -1 tails in the gathered lists are skipped, output padded."""
+    import torch
+    from image_recommender_amd.sharded import merge_gathered_device
+    xb = mixture(9, 16, seed=4)
+    gD = torch.empty((3, 2, 6), dtype=torch.float32, device="cuda")
+    gI = torch.empty((3, 2, 6), dtype=torch.int64, device="cuda")
+    q = torch.from_numpy(xb[:2].copy()).cuda()
+    for r in range(3):
+        sh = faiss.IndexFlatL2(16)
+        sh.set_id_offset(3 * r)
+        sh.add(xb[3 * r:3 * r + 3])
+        sh.search_device(q.data_ptr(), 2, 6, gD[r].data_ptr(), gI[r].data_ptr(), 0)
+    D, I = merge_gathered_device(gD, gI, 12, faiss.METRIC_L2)
+    I = I.cpu().numpy()
+    assert (I[:, 9:] == -1).all() and sorted(I[0, :9].tolist()) == list(range(9))
+    assert (D.cpu().numpy()[:, 9:] == np.finfo(np.float32).max).all()
+    check_knn(D.cpu().numpy()[:, :9], I[:, :9], xb, xb[:2], 9, "l2")
