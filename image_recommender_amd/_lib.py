@@ -57,6 +57,7 @@ SIGNATURES = {
     # imgrec_ingest.h
     "ingest_parse_f32": (_i64, [_vp, _i64, _vp, _i64]),
     "ingest_concat_rows": (_i64, [C.POINTER(_vp), _pi64, _i64, _i, _pi64, _vp, _vp]),
+    "ingest_concat_packed": (_i64, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp]),
 }
 
 

@@ -154,4 +154,32 @@ int64_t ingest_concat_rows(const uint8_t* const* blobs, const int64_t* lens, int
     return good;
 }
 
+int64_t ingest_concat_packed(const uint8_t* buf, const int64_t* offsets, const int64_t* lens,
+                             int64_t nrows, int nparts, const int64_t* part_dims, float* out,
+                             int8_t* status) {
+    int64_t D = 0;
+    for (int j = 0; j < nparts; ++j) D += part_dims[j];
+    int64_t good = 0;
+    for (int64_t r = 0; r < nrows; ++r) {
+        float* o = out + r * D;
+        int8_t st = 0;
+        for (int j = 0; j < nparts && st == 0; ++j) {
+            const uint8_t* pl;
+            int64_t nb, ne;
+            const int64_t k = r * nparts + j;
+            if (lens[k] < 0 || !parse(buf + offsets[k], lens[k], &pl, &nb, &ne)) {
+                st = 1;
+            } else if (ne != part_dims[j]) {
+                st = 2;
+            } else {
+                memcpy(o, pl, (size_t)nb);
+                o += ne;
+            }
+        }
+        status[r] = st;
+        if (st == 0) ++good;
+    }
+    return good;
+}
+
 }  // extern "C"

@@ -397,13 +397,15 @@ int knn_merge_device(const float* cD, const int64_t* cI, int nlists, int64_t nq,
 
 int knn_normalize_L2(float* x, int64_t n, int d) {
     if (n < 0 || d <= 0 || (n > 0 && !x)) KNN_FAIL(KNN_EINVAL, "bad array");
-    // faiss fvec_renorm_L2: per row, nr = |x|^2 (float); if nr > 0: x *= (float)(1.0 / sqrtf(nr)).
+    // faiss fvec_renorm_L2: per row, nr = |x|^2; if nr > 0: x *= 1 / sqrt(nr).  The norm is
+    // accumulated in double here (faiss sums in float SIMD lanes), so the scale is the correctly
+    // rounded reciprocal norm and each output is within ~1 ulp of x / |x|.
     for (int64_t i = 0; i < n; ++i) {
         float* r = x + i * (int64_t)d;
-        float nr = 0.f;
-        for (int j = 0; j < d; ++j) nr += r[j] * r[j];
-        if (nr > 0.f) {
-            const float s = (float)(1.0 / (double)sqrtf(nr));
+        double nr = 0.0;
+        for (int j = 0; j < d; ++j) nr += (double)r[j] * (double)r[j];
+        if (nr > 0.0) {
+            const float s = (float)(1.0 / sqrt(nr));
             for (int j = 0; j < d; ++j) r[j] *= s;
         }
     }

@@ -238,38 +238,57 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     const float* qbase = qp + (size_t)qb * BQ * dp;
 
     // ---- DMA issue cursor (runs NS-1 stages ahead of the consumer) -------------------------
+    // Piece j of this wave is piece pc = wave*LPW + j of a stage: an A piece (16 corpus rows of
+    // the tile) or a B piece (16 queries).  Its source is base + tile offset + 16*stage floats;
+    // the per-piece offsets are wave-uniform constants, so each issue is a few scalar adds.
+    int64_t poff[LPW];
+    bool pis_a[LPW];
+    uint32_t pdst[LPW];
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+        const int pc = wave * LPW + j;
+        pis_a[j] = pc < PA;
+        poff[j] = pis_a[j] ? (int64_t)pc * 16 * dp : (int64_t)(pc - PA) * 16 * dp;
+        pdst[j] = (uint32_t)(pis_a[j] ? pc * 256 : SA + (pc - PA) * 256) * 4u;
+    }
+    const uint32_t smem_u32 = lds_addr(smem);
+    const uint32_t norm_u32 = lds_addr(norm_base);
     int it = t0, is = 0, ibuf = 0;
-    auto issue_next = [&]() __attribute__((always_inline)) {
-        if (it >= t1) return;
-        const uint32_t st = lds_addr(smem) + (uint32_t)(ibuf * STAGE) * 4u;
+    const float* itile = xb + (size_t)t0 * BM * dp;     // corpus rows of tile `it`
+    // Issue is split so the 1-KiB DMA instructions can be spread between MFMAs (an LDS-DMA
+    // piece costs ~100+ issue cycles; behind it in program order the MFMAs would wait).
+    bool do_issue = false;
+    uint32_t ist = 0;
+    int ik0 = 0;
+    auto issue_begin = [&]() __attribute__((always_inline)) {
+        do_issue = it < t1;
+        if (!do_issue) return;
+        ist = smem_u32 + (uint32_t)(ibuf * STAGE) * 4u;
         if (is == 0) {                      // row norms of the tile, one 4-B DMA per lane
             for (int j = wave; j < BM / 64; j += NW)
                 dma4(xnorm + (size_t)it * BM + j * 64 + lane,
-                     lds_addr(norm_base) + (uint32_t)(((it - t0) % NS) * BM + j * 64) * 4u);
+                     norm_u32 + (uint32_t)(((it - t0) % NS) * BM + j * 64) * 4u);
         }
-        const int k0 = is * BK;
-#pragma unroll
-        for (int j = 0; j < LPW; ++j) {
-            const int pc = wave * LPW + j;      // wave-uniform
-            const float* src;
-            uint32_t dst;
-            if (pc < PA) {
-                src = xb + ((size_t)it * BM + pc * 16) * dp + k0 + goff;
-                dst = st + (uint32_t)(pc * 256) * 4u;
-            } else {
-                src = qbase + (size_t)(pc - PA) * 16 * dp + k0 + goff;
-                dst = st + (uint32_t)(SA + (pc - PA) * 256) * 4u;
-            }
-            dma16(src, dst);
-        }
-        if (++is == nsteps) { is = 0; ++it; }
+        ik0 = is * BK;
+    };
+    auto issue_piece = [&](int j) __attribute__((always_inline)) {
+        if (do_issue) dma16((pis_a[j] ? itile : qbase) + poff[j] + ik0 + goff, ist + pdst[j]);
+    };
+    auto issue_end = [&]() __attribute__((always_inline)) {
+        if (!do_issue) return;
+        if (++is == nsteps) { is = 0; ++it; itile += (size_t)BM * dp; }
         ibuf = (ibuf + 1 == NS) ? 0 : ibuf + 1;
+    };
+    auto issue_next = [&]() __attribute__((always_inline)) {
+        issue_begin();
+#pragma unroll
+        for (int j = 0; j < LPW; ++j) issue_piece(j);
+        issue_end();
     };
 
 #pragma unroll
     for (int j = 0; j < NS - 1; ++j) issue_next();
-    const int64_t total = (int64_t)(t1 - t0) * nsteps;
-    int64_t g = 0;
+    int remaining = (t1 - t0) * nsteps;     // stages not yet consumed (fits: < 2^31)
     int cbuf = 0;
 
     for (int t = t0; t < t1; ++t) {
@@ -278,14 +297,17 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[b] = (f32x16){0.f};
 
-        for (int s = 0; s < nsteps; ++s, ++g) {
-            // own DMA of stage g landed (loads of the stages issued after it may stay in flight)
-            const int64_t ahead = total - 1 - g;     // stages after g that have been issued
-            if (ahead >= NS - 2) wait_vmcnt<LPW * (NS - 2)>();
-            else if (NS > 3 && ahead == 1) wait_vmcnt<LPW>();
+        for (int s = 0; s < nsteps; ++s) {
+            // own DMA of this stage landed (later stages may stay in flight)
+            --remaining;                             // stages issued after this one: min(NS-2, remaining)
+#ifdef IMGREC_ABLATE_NO_WAIT
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+            if (remaining >= NS - 2) wait_vmcnt<LPW * (NS - 2)>();
+            else if (NS > 3 && remaining == 1) wait_vmcnt<LPW>();
             else wait_vmcnt<0>();
-            barrier_raw();                           // everyone's DMA landed; stage g-1 fully read
-            issue_next();                            // refills the buffer stage g-1 used
+#endif
+            barrier_raw();                           // everyone's DMA landed; previous stage read
 
             const float* st = smem + cbuf * STAGE;
             cbuf = (cbuf + 1 == NS) ? 0 : cbuf + 1;
@@ -305,12 +327,31 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                 a[b][0] = a0.x; a[b][1] = a0.y; a[b][2] = a0.z; a[b][3] = a0.w;
                 a[b][4] = a1.x; a[b][5] = a1.y; a[b][6] = a1.z; a[b][7] = a1.w;
             }
+#ifndef IMGREC_ABLATE_NO_DMA
+            issue_begin();                           // refills the buffer the previous stage used
+#endif
+            // The stage's DMA pieces go out right after the fragment reads (their address math
+            // overlaps the LDS latency), before the MFMAs.  Measured alternatives, all slower on
+            // 1M x 1968 x 1024: pieces pinned between MFMAs (38.6 ms vs 33.5), staggered per wave
+            // (38.8), a 5-deep ring (39.0).
+#ifndef IMGREC_ABLATE_NO_DMA
+#pragma unroll
+            for (int j = 0; j < LPW; ++j) {
+#ifdef IMGREC_ABLATE_A_ONLY
+                if (pis_a[j])
+#endif
+                issue_piece(j);
+            }
+#endif
 #pragma unroll
             for (int kk = 0; kk < 8; ++kk) {
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
             }
+#ifndef IMGREC_ABLATE_NO_DMA
+            issue_end();
+#endif
         }
 
         // ---- epilogue: key = L2 distance (faiss exhaustive_L2sqr_blas form, clamped at 0) or
@@ -520,7 +561,10 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
-    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, 4>(a.km, a, st);
+#ifndef IMGREC_NS_BIG
+#define IMGREC_NS_BIG 4
+#endif
+    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, IMGREC_NS_BIG>(a.km, a, st);
     if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2, 3>(a.km, a, st);
     if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1, 3>(a.km, a, st);
     return hipErrorInvalidValue;

@@ -30,6 +30,12 @@ int64_t ingest_parse_f32(const uint8_t* blob, int64_t len, float* out, int64_t c
 int64_t ingest_concat_rows(const uint8_t* const* blobs, const int64_t* lens, int64_t nrows,
                            int nparts, const int64_t* part_dims, float* out, int8_t* status);
 
+/* Same, with all BLOBs packed back to back in one buffer: BLOB (row, part) occupies
+ * buf[offsets[row*nparts+part] .. + lens[row*nparts+part]) (a length < 0 marks a NULL BLOB). */
+int64_t ingest_concat_packed(const uint8_t* buf, const int64_t* offsets, const int64_t* lens,
+                             int64_t nrows, int nparts, const int64_t* part_dims, float* out,
+                             int8_t* status);
+
 #ifdef __cplusplus
 }
 #endif

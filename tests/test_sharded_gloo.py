@@ -1,0 +1,88 @@
+"""Multi-process (world size 2 and 3, gloo, CPU) test of the row-sharded search protocol (§8e).
+
+What runs on the GPU in production — each shard's fused search and the final merge — is replaced
+by the float64 oracle here; everything else is the product code: ``shard_range`` (contiguous
+balanced row ranges, labels = global offsets), ``gather_results`` (the all-gather into the
+[world][nq][k] layout that knn_merge_device consumes).  The merged result must equal an unsharded
+search of the whole corpus, labels included.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.datagen import mixture
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _merge_oracle(gD, gI, k, metric):
+    """Reference semantics of knn_merge_device: best k of the gathered lists by (key, label)."""
+    world, nq, kin = gD.shape
+    D = np.empty((nq, k), np.float64)
+    I = np.empty((nq, k), np.int64)
+    for q in range(nq):
+        d = gD[:, q, :].reshape(-1)
+        i = gI[:, q, :].reshape(-1)
+        ok = i >= 0
+        key = d[ok] if metric == "l2" else -d[ok]
+        order = np.lexsort((i[ok], key))[:k]
+        n = len(order)
+        D[q, :n], I[q, :n] = d[ok][order], i[ok][order]
+        D[q, n:], I[q, n:] = (np.finfo(np.float32).max if metric == "l2" else -np.finfo(np.float32).max), -1
+    return D, I
+
+
+def _worker(rank, world, port, n, d, nq, k, metric, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from image_recommender_amd.sharded import gather_results, shard_range
+        from oracle.flat_knn import search_exact
+        xb = mixture(n, d, centres=30, seed=11)
+        xq = mixture(nq, d, centres=30, seed=12)
+        r0, r1 = shard_range(n, rank, world)
+        D, I = search_exact(xb[r0:r1], xq, k, metric)
+        I = np.where(I >= 0, I + r0, -1)                # knn_set_id_offset(r0)
+        gD, gI = gather_results(torch.from_numpy(D), torch.from_numpy(I))
+        Dm, Im = _merge_oracle(gD.numpy(), gI.numpy(), k, metric)
+        if rank == 0:
+            out.put((Dm, Im, [shard_range(n, r, world) for r in range(world)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,k,metric", [(2, 3001, 10, "l2"), (3, 1000, 7, "ip"),
+                                              (2, 5, 8, "l2")])
+def test_row_sharded_search_equals_unsharded(world, n, k, metric):
+    from oracle.flat_knn import search_exact
+    ctx = mp.get_context("spawn")
+    out = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 24, 9, k, metric, out))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    Dm, Im, ranges = out.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # contiguous, balanced, covering
+    assert ranges[0][0] == 0 and ranges[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    assert max(r1 - r0 for r0, r1 in ranges) - min(r1 - r0 for r0, r1 in ranges) <= 1
+    xb = mixture(n, 24, centres=30, seed=11)
+    xq = mixture(9, 24, centres=30, seed=12)
+    D, I = search_exact(xb, xq, k, metric)
+    np.testing.assert_array_equal(Im, I)
+    np.testing.assert_allclose(Dm, D, rtol=0, atol=0)
