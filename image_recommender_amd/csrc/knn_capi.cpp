@@ -244,7 +244,8 @@ int knn_create(int d, int metric, int device, knn_index_t** out) {
     DeviceGuard g(device);
     knn_index* ix = new knn_index();
     ix->d = d;
-    ix->dp = (int)round_up(d, imgrec::kDepthPad);
+    // rows padded to 16 floats; from d >= 512 to 32 so the 32-deep staging path applies
+    ix->dp = (int)round_up(d, d >= 512 ? 2 * imgrec::kDepthPad : imgrec::kDepthPad);
     ix->metric = metric;
     ix->device = device;
     int cus = 0;

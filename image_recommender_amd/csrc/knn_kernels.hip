@@ -105,32 +105,36 @@ rows_ingest_kernel(const float* __restrict__ src, int64_t n, int d, int dp, int6
 // Workgroup = WR x WQ waves; wave tile = 128 corpus rows (4 MFMA row blocks) x 32 queries, so the
 // workgroup tile is BM = 128*WR rows x BQ = 32*WQ queries.  A workgroup owns one query block and a
 // contiguous range of row tiles (a "row split") and streams it as one continuous sequence of
-// 16-deep K stages: (tile t0, stage 0..nsteps-1), (t0+1, 0..), ...
+// BK-deep K stages: (tile t0, stage 0..nsteps-1), (t0+1, 0..), ...
 //
-// Staging is LDS-DMA (global_load_lds_dwordx4): each wave instruction moves one 1-KiB piece =
-// 16 rows x 64 B straight into LDS (no staging VGPRs), into an NS-deep ring; a stage is read NS-1
-// iterations after its loads were issued, behind a counted `s_waitcnt vmcnt` and one raw
+// Staging is LDS-DMA (global_load_lds_dwordx4): each wave instruction moves one 1-KiB piece
+// (RPP rows x 4*BK bytes) straight into LDS, no staging VGPRs, into an NS-deep ring; a stage is
+// read NS-1 iterations after its loads were issued, behind a counted `s_waitcnt vmcnt` and one raw
 // s_barrier per stage (cdna_hip_programming.md §5 "Pipelining across barriers").  The ring runs
-// across tile boundaries, so the top-k epilogue of a tile overlaps the next tile's loads.
+// across tile boundaries, so a tile's top-k epilogue overlaps the next tile's loads.
 //
-// LDS image: rows of 16 floats (64 B), 16-B chunk c of row r stored at chunk c ^ ((r >> 2) & 3).
-// The XOR is applied to the per-lane GLOBAL source address (the DMA destination is lane-linear);
-// the fragment reads apply the same XOR, which makes every ds_read_b128 16-lane group hit 16
-// distinct 16-B bank slots.
+// LDS image: rows of BK floats; 16-B chunk c of row r stored at chunk c ^ ((r / RPB) % CPR)
+// (RPB = rows per 256-B bank row, CPR = chunks per row).  The XOR is applied to the per-lane
+// GLOBAL source address (the DMA destination is lane-linear); the fragment reads apply the same
+// XOR, which makes every ds_read_b128 16-lane group hit 16 distinct 16-B bank slots.
 // ---------------------------------------------------------------------------------------------
-constexpr int BK = 16;     // depth of one stage (floats)
-
-template <int WR, int WQ, int NS>
+template <int WR, int WQ, int NS, int BK>
 struct TileGeom {
     static constexpr int NW = WR * WQ, NT = NW * 64;
     static constexpr int BM = WR * 128, BQ = WQ * 32;
+    static constexpr int CPR = BK / 4;                 // 16-B chunks per staged row
+    static constexpr int RPP = 64 / CPR;               // rows per 1-KiB DMA piece
+    static constexpr int RPB = 64 / BK;                // rows per 256-B bank row
     static constexpr int SA = BM * BK, SB = BQ * BK, STAGE = SA + SB;   // floats
-    static constexpr int PA = BM / 16, PB = BQ / 16, PIECES = PA + PB;  // 1-KiB pieces / stage
-    static constexpr int LPW = PIECES / NW;                            // pieces per wave
-    static constexpr int PARK = NW * 16 * 64;                          // epilogue key parking
-    static constexpr int LDS_FLOATS = NS * STAGE + PARK + NS * BM;
+    static constexpr int PA = BM / RPP, PB = BQ / RPP, PIECES = PA + PB;
+    static constexpr int LPW = PIECES / NW;            // pieces per wave per stage
+    static constexpr int PARK = NW * 8 * 64;           // epilogue key parking (in a spent stage)
+    static constexpr int LDS_FLOATS = NS * STAGE + NS * BM;
+    static_assert(BK == 16 || BK == 32, "stage depth");
     static_assert(PIECES % NW == 0, "pieces must divide evenly over waves");
     static_assert(BM % 64 == 0, "norm DMA uses whole waves");
+    static_assert(STAGE >= PARK, "epilogue parking must fit in one stage");
+    static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
 };
 
 // LDS byte address of a pointer into __shared__ memory.
@@ -147,14 +151,14 @@ __device__ __forceinline__ void dma16(const float* g, uint32_t lds) {
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
         "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+        : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
 }
 __device__ __forceinline__ void dma4(const float* g, uint32_t lds) {
     unsigned keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
         "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+        : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
 }
 
 template <int N>
@@ -185,19 +189,19 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
     ki[0] = here0 ? id : ki[0];
 }
 
-template <int WR, int WQ, int KM, int NS>
+template <int WR, int WQ, int KM, int NS, int BK>
 __global__ void __launch_bounds__(WR * WQ * 64)
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
                      int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
                      int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
                      float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand) {
-    using G = TileGeom<WR, WQ, NS>;
+    using G = TileGeom<WR, WQ, NS, BK>;
     constexpr int NW = G::NW, BM = G::BM, BQ = G::BQ, SA = G::SA, STAGE = G::STAGE;
-    constexpr int PA = G::PA, LPW = G::LPW;
+    constexpr int PA = G::PA, LPW = G::LPW, CPR = G::CPR, RPP = G::RPP, RPB = G::RPB;
+    constexpr int KH = BK / 2;          // MFMA sub-steps per stage (each covers depth 2)
 
     __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
-    float* const park_base = smem + NS * STAGE;
-    float* const norm_base = park_base + G::PARK;
+    float* const norm_base = smem + NS * STAGE;
 
     // XCD-aware, bijective block -> (query block, row split) map: blocks b and b+8 share an XCD;
     // consecutive remapped ids (same XCD) share a row split, so the corpus stages they stream are
@@ -222,12 +226,16 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     float qn = (metric == 1) ? qnorm[qcol] : 0.f;
     asm volatile("" : "+v"(qn));   // consume the load here, before the DMA stream starts
 
-    // per-lane DMA source offset inside a piece: row (lane >> 2), logical chunk swizzled
-    const int goff = (lane >> 2) * dp + 4 * ((lane & 3) ^ ((lane >> 4) & 3));
-    // per-lane fragment offsets inside a 32-row block: logical chunks 2h, 2h+1 of row li
-    const int sw = (li >> 2) & 3;
-    const int fo0 = li * BK + 4 * ((2 * lh) ^ sw);
-    const int fo1 = li * BK + 4 * ((2 * lh + 1) ^ sw);
+    // per-lane DMA source offsets inside a piece (row lane/CPR, logical chunk swizzled); the
+    // swizzle of a piece's rows depends on the piece index modulo 64/(RPP*...) -> two variants.
+    const int prow = lane / CPR, pchk = lane % CPR;
+    const int goff0 = prow * dp + 4 * (pchk ^ (((0 * RPP + prow) / RPB) % CPR));
+    const int goff1 = prow * dp + 4 * (pchk ^ (((1 * RPP + prow) / RPB) % CPR));
+    // per-lane fragment offsets inside a 32-row block: logical chunks lh*CPR/2 + c of row li
+    const int fsw = (li / RPB) % CPR;
+    int fo[CPR / 2];
+#pragma unroll
+    for (int c = 0; c < CPR / 2; ++c) fo[c] = li * BK + 4 * ((lh * (CPR / 2) + c) ^ fsw);
 
     float kd[KM];
     int ki[KM];
@@ -238,9 +246,8 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     const float* qbase = qp + (size_t)qb * BQ * dp;
 
     // ---- DMA issue cursor (runs NS-1 stages ahead of the consumer) -------------------------
-    // Piece j of this wave is piece pc = wave*LPW + j of a stage: an A piece (16 corpus rows of
-    // the tile) or a B piece (16 queries).  Its source is base + tile offset + 16*stage floats;
-    // the per-piece offsets are wave-uniform constants, so each issue is a few scalar adds.
+    // Piece j of this wave is piece pc = wave*LPW + j of a stage: an A piece (RPP corpus rows of
+    // the tile) or a B piece (RPP queries).  Its source is base + tile offset + BK*stage floats.
     int64_t poff[LPW];
     bool pis_a[LPW];
     uint32_t pdst[LPW];
@@ -248,47 +255,37 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     for (int j = 0; j < LPW; ++j) {
         const int pc = wave * LPW + j;
         pis_a[j] = pc < PA;
-        poff[j] = pis_a[j] ? (int64_t)pc * 16 * dp : (int64_t)(pc - PA) * 16 * dp;
+        const int prow0 = pis_a[j] ? pc * RPP : (pc - PA) * RPP;
+        poff[j] = (int64_t)prow0 * dp + (((prow0 / RPP) & 1) ? goff1 : goff0);
         pdst[j] = (uint32_t)(pis_a[j] ? pc * 256 : SA + (pc - PA) * 256) * 4u;
     }
     const uint32_t smem_u32 = lds_addr(smem);
     const uint32_t norm_u32 = lds_addr(norm_base);
     int it = t0, is = 0, ibuf = 0;
     const float* itile = xb + (size_t)t0 * BM * dp;     // corpus rows of tile `it`
-    // Issue is split so the 1-KiB DMA instructions can be spread between MFMAs (an LDS-DMA
-    // piece costs ~100+ issue cycles; behind it in program order the MFMAs would wait).
-    bool do_issue = false;
-    uint32_t ist = 0;
-    int ik0 = 0;
-    auto issue_begin = [&]() __attribute__((always_inline)) {
-        do_issue = it < t1;
-        if (!do_issue) return;
-        ist = smem_u32 + (uint32_t)(ibuf * STAGE) * 4u;
+    auto issue_next = [&]() __attribute__((always_inline)) {
+        if (it >= t1) return;
+        const uint32_t st = smem_u32 + (uint32_t)(ibuf * STAGE) * 4u;
         if (is == 0) {                      // row norms of the tile, one 4-B DMA per lane
             for (int j = wave; j < BM / 64; j += NW)
                 dma4(xnorm + (size_t)it * BM + j * 64 + lane,
                      norm_u32 + (uint32_t)(((it - t0) % NS) * BM + j * 64) * 4u);
         }
-        ik0 = is * BK;
-    };
-    auto issue_piece = [&](int j) __attribute__((always_inline)) {
-        if (do_issue) dma16((pis_a[j] ? itile : qbase) + poff[j] + ik0 + goff, ist + pdst[j]);
-    };
-    auto issue_end = [&]() __attribute__((always_inline)) {
-        if (!do_issue) return;
+        const int k0 = is * BK;
+#pragma unroll
+        for (int j = 0; j < LPW; ++j) {
+#ifdef IMGREC_ABLATE_A_ONLY
+            if (pis_a[j])
+#endif
+            dma16((pis_a[j] ? itile : qbase) + poff[j] + k0, st + pdst[j]);
+        }
         if (++is == nsteps) { is = 0; ++it; itile += (size_t)BM * dp; }
         ibuf = (ibuf + 1 == NS) ? 0 : ibuf + 1;
-    };
-    auto issue_next = [&]() __attribute__((always_inline)) {
-        issue_begin();
-#pragma unroll
-        for (int j = 0; j < LPW; ++j) issue_piece(j);
-        issue_end();
     };
 
 #pragma unroll
     for (int j = 0; j < NS - 1; ++j) issue_next();
-    int remaining = (t1 - t0) * nsteps;     // stages not yet consumed (fits: < 2^31)
+    int remaining = (t1 - t0) * nsteps;     // stages not yet consumed
     int cbuf = 0;
 
     for (int t = t0; t < t1; ++t) {
@@ -297,6 +294,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[b] = (f32x16){0.f};
 
+        const float* st = smem;
         for (int s = 0; s < nsteps; ++s) {
             // own DMA of this stage landed (later stages may stay in flight)
             --remaining;                             // stages issued after this one: min(NS-2, remaining)
@@ -309,62 +307,57 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #endif
             barrier_raw();                           // everyone's DMA landed; previous stage read
 
-            const float* st = smem + cbuf * STAGE;
+            st = smem + cbuf * STAGE;
             cbuf = (cbuf + 1 == NS) ? 0 : cbuf + 1;
-            float a[4][8], bq[8];
+            float a[4][KH], bq[KH];
             {
                 const float* bp = st + SA + wq * 32 * BK;
-                const float4 b0 = *reinterpret_cast<const float4*>(bp + fo0);
-                const float4 b1 = *reinterpret_cast<const float4*>(bp + fo1);
-                bq[0] = b0.x; bq[1] = b0.y; bq[2] = b0.z; bq[3] = b0.w;
-                bq[4] = b1.x; bq[5] = b1.y; bq[6] = b1.z; bq[7] = b1.w;
+#pragma unroll
+                for (int c = 0; c < CPR / 2; ++c) {
+                    const float4 v = *reinterpret_cast<const float4*>(bp + fo[c]);
+                    bq[4 * c] = v.x; bq[4 * c + 1] = v.y; bq[4 * c + 2] = v.z; bq[4 * c + 3] = v.w;
+                }
             }
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const float* ap = st + (wr * 128 + b * 32) * BK;
-                const float4 a0 = *reinterpret_cast<const float4*>(ap + fo0);
-                const float4 a1 = *reinterpret_cast<const float4*>(ap + fo1);
-                a[b][0] = a0.x; a[b][1] = a0.y; a[b][2] = a0.z; a[b][3] = a0.w;
-                a[b][4] = a1.x; a[b][5] = a1.y; a[b][6] = a1.z; a[b][7] = a1.w;
+#pragma unroll
+                for (int c = 0; c < CPR / 2; ++c) {
+                    const float4 v = *reinterpret_cast<const float4*>(ap + fo[c]);
+                    a[b][4 * c] = v.x; a[b][4 * c + 1] = v.y; a[b][4 * c + 2] = v.z; a[b][4 * c + 3] = v.w;
+                }
             }
-#ifndef IMGREC_ABLATE_NO_DMA
-            issue_begin();                           // refills the buffer the previous stage used
-#endif
             // The stage's DMA pieces go out right after the fragment reads (their address math
-            // overlaps the LDS latency), before the MFMAs.  Measured alternatives, all slower on
-            // 1M x 1968 x 1024: pieces pinned between MFMAs (38.6 ms vs 33.5), staggered per wave
-            // (38.8), a 5-deep ring (39.0).
+            // overlaps the LDS latency), before the MFMAs.  Measured alternatives, all slower:
+            // pieces pinned between MFMAs (38.6 ms vs 33.5 at BK=16), staggered per wave (38.8),
+            // a 5-deep ring (39.0).
 #ifndef IMGREC_ABLATE_NO_DMA
-#pragma unroll
-            for (int j = 0; j < LPW; ++j) {
-#ifdef IMGREC_ABLATE_A_ONLY
-                if (pis_a[j])
-#endif
-                issue_piece(j);
-            }
+            issue_next();                            // refills the buffer the previous stage used
 #endif
 #pragma unroll
-            for (int kk = 0; kk < 8; ++kk) {
+            for (int kk = 0; kk < KH; ++kk) {
 #pragma unroll
                 for (int b = 0; b < 4; ++b)
                     acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
             }
-#ifndef IMGREC_ABLATE_NO_DMA
-            issue_end();
-#endif
         }
 
         // ---- epilogue: key = L2 distance (faiss exhaustive_L2sqr_blas form, clamped at 0) or
         // -ip; screened against this lane's K-th key and (<=) its partner lane's K-th key (the
         // partner holds the same query's other rows: a key worse than the partner's K-th cannot
-        // reach the union's top K).  Survivors are parked in per-wave LDS and inserted one by one.
+        // reach the union's top K).  Survivors are parked in the stage this tile just consumed
+        // (refilled only after the next barrier, which every wave reaches after its epilogue)
+        // and inserted one by one.
+        // every wave (all lanes: qvalid is per lane) passes this barrier exactly once per tile
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        barrier_raw();                               // all fragment reads of the spent stage done
 #ifdef IMGREC_ABLATE_NO_EPILOGUE
         if (qvalid && row0 < 0) {   // never taken: keeps the accumulators live, no top-k work
 #else
         if (qvalid) {
 #endif
             const float* nrm = norm_base + ((t - t0) % NS) * BM;
-            float* park = park_base + wave * (16 * 64);
+            float* park = const_cast<float*>(st) + wave * (8 * 64);
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 float key[16];
@@ -386,15 +379,21 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                     const bool pass = (row0 + rl < nrows) && kv < tau && kv <= tau_p;
                     mask |= (unsigned)pass << r;
                 }
-                if (__any(mask != 0)) {
+                // two parking rounds of 8 keys (the park must fit in one spent stage)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) park[r * 64 + lane] = key[r];
+                for (int h8 = 0; h8 < 2; ++h8) {
+                    const unsigned m8 = (mask >> (8 * h8)) & 0xffu;
+                    if (__any(m8 != 0)) {
+#pragma unroll
+                        for (int r = 0; r < 8; ++r) park[r * 64 + lane] = key[8 * h8 + r];
 #pragma unroll 1
-                    for (int r = 0; r < 16; ++r) {
-                        if ((mask >> r) & 1u) {
-                            const float kv = park[r * 64 + lane];
-                            const int row = row0 + wr * 128 + b * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                            if (kv < kd[KM - 1]) list_insert_mono<KM>(kd, ki, kv, row);
+                        for (int r = 0; r < 8; ++r) {
+                            if ((m8 >> r) & 1u) {
+                                const float kv = park[r * 64 + lane];
+                                const int rr8 = 8 * h8 + r;
+                                const int row = row0 + wr * 128 + b * 32 + (rr8 & 3) + 8 * (rr8 >> 2) + 4 * lh;
+                                if (kv < kd[KM - 1]) list_insert_mono<KM>(kd, ki, kv, row);
+                            }
                         }
                     }
                 }
@@ -542,11 +541,11 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
     return hipGetLastError();
 }
 
-template <int WR, int WQ, int NS>
+template <int WR, int WQ, int NS, int BK>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
-    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS>), grid, block, 0, st, a.xb,         \
+    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK>), grid, block, 0, st, a.xb,     \
                        a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
                        a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
     switch (km) {
@@ -560,13 +559,19 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
-#ifndef IMGREC_NS_BIG
-#define IMGREC_NS_BIG 4
+#ifndef IMGREC_BK_BIG
+#define IMGREC_BK_BIG 32
 #endif
-    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, IMGREC_NS_BIG>(a.km, a, st);
-    if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2, 3>(a.km, a, st);
-    if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1, 3>(a.km, a, st);
+#ifndef IMGREC_NS_BIG
+#define IMGREC_NS_BIG 3
+#endif
+
+hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
+    if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)
+        return launch_tile_km<1, 8, 4, 16>(a.km, a, st);
+    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, IMGREC_NS_BIG, IMGREC_BK_BIG>(a.km, a, st);
+    if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2, 3, 16>(a.km, a, st);
+    if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1, 3, 16>(a.km, a, st);
     return hipErrorInvalidValue;
 }
 
