@@ -177,6 +177,22 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
     }
 
 
+def pmc_traffic(kernel_prefix: str):
+    """HBM bytes per launch of the fused kernel from the newest profiles/*_traffic.json written by
+    tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            data = json.load(open(f))
+        except Exception:
+            continue
+        for name, rec in data.items():
+            if name.startswith(kernel_prefix):
+                return rec["hbm_bytes_per_launch"], os.path.basename(f)
+    return None
+
+
 def main():
     a = parse()
     import torch
@@ -284,6 +300,8 @@ def main():
     if rank == 0:
         n_local = shard.local_rows
         flops = 2.0 * n_local * D_total * a.nq
+        kname = f"void imgrec::knn_tile_topk_kernel<{tr.value // 128}, {tq.value // 32}"
+        traffic = pmc_traffic(kname) if world == 1 else None
         achieved = flops / (kern_ms * 1e-3) / 1e12
         bytes1 = 4.0 * n_local * D_total + 4.0 * n_local
         qps = a.nq * a.steps / elapsed
@@ -312,8 +330,11 @@ def main():
             "max_abs_dist_err_vs_fp64": max_dist_err,
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS, "traffic": None,
-                "kernel": "knn_tile_topk_kernel<1,8,16>", "kernel_ms": kern_ms,
+                "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS,
+                "traffic": traffic[0] if traffic else None,
+                "traffic_source": traffic[1] if traffic else None,
+                "kernel": f"knn_tile_topk_kernel<{tr.value // 128},{tq.value // 32},...>",
+                "kernel_ms": kern_ms,
                 "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
             },
             "single_query": {

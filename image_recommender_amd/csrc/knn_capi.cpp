@@ -85,7 +85,13 @@ Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
     int wg_per_cu;
     if (nq <= 32) { p.wr = 2; p.wq = 1; wg_per_cu = 3; }
     else if (nq <= 128) { p.wr = 2; p.wq = 2; wg_per_cu = 2; }
-    else { p.wr = 1; p.wq = 8; wg_per_cu = 1; }
+#ifdef IMGREC_BIG_TILE_18
+    else { p.wr = 1; p.wq = 8; wg_per_cu = 1; }   // one 8-wave workgroup per CU (32.2 ms, ablation)
+#else
+    // Two independent 4-wave workgroups per CU: their barriers do not line up, so one
+    // workgroup's stage bubble is filled by the other's MFMAs (31.4 vs 32.2 ms, bench config).
+    else { p.wr = 1; p.wq = 4; wg_per_cu = 2; }
+#endif
     p.bm = p.wr * 128;
     p.bq = p.wq * 32;
     p.nqb = (int)((nq + p.bq - 1) / p.bq);

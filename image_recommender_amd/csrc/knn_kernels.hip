@@ -570,6 +570,8 @@ hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
     if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)
         return launch_tile_km<1, 8, 4, 16>(a.km, a, st);
     if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, IMGREC_NS_BIG, IMGREC_BK_BIG>(a.km, a, st);
+    if (a.wr == 1 && a.wq == 4 && a.dp % 32 == 0) return launch_tile_km<1, 4, 2, 32>(a.km, a, st);
+    if (a.wr == 1 && a.wq == 4) return launch_tile_km<1, 4, 2, 16>(a.km, a, st);
     if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2, 3, 16>(a.km, a, st);
     if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1, 3, 16>(a.km, a, st);
     return hipErrorInvalidValue;
