@@ -32,6 +32,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2516.8   # dense bf16 MFMA peak = 16 x the f32 rate (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0            # MI355X HBM3E peak (spec)
 BLOCK = 16384                    # rows per generation block (the seed unit)
 
@@ -57,6 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--single-query-steps", type=int, default=50)
+    ap.add_argument("--mode", choices=("auto", "exact", "split"), default="auto",
+                    help="search arithmetic (include/imgrec_knn.h knn_search_mode)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed steps (for rocprofv3 runs)")
     return ap.parse_args()
@@ -177,7 +180,7 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
     }
 
 
-def pmc_traffic(kernel_prefix: str):
+def pmc_traffic(kernel_prefix: str, split: bool):
     """HBM bytes per launch of the fused kernel from the newest profiles/*_traffic.json written by
     tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None."""
     import glob
@@ -188,7 +191,7 @@ def pmc_traffic(kernel_prefix: str):
         except Exception:
             continue
         for name, rec in data.items():
-            if name.startswith(kernel_prefix):
+            if name.startswith(kernel_prefix) and name.endswith("true>" if split else "false>"):
                 return rec["hbm_bytes_per_launch"], os.path.basename(f)
     return None
 
@@ -227,6 +230,7 @@ def main():
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t_build0
     lib = _lib.load()
+    shard.index.search_mode = a.mode
 
     def step():
         return shard.search(q, a.k)
@@ -245,6 +249,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    split_q, fallback_q, err_ratio = shard.index.search_stats(with_error=True)   # last step
     import ctypes as C
     tot_ms, nl = C.c_double(), C.c_int()
     _lib.check(lib.knn_kernel_time(shard.index.handle, C.byref(tot_ms), C.byref(nl)), "timing")
@@ -255,7 +260,8 @@ def main():
     elapsed, kern_ms = float(el[0]), float(el[1])
     if a.profile_only:
         if rank == 0:
-            print(json.dumps({"elapsed_s": elapsed, "kernel_ms": kern_ms}))
+            print(json.dumps({"elapsed_s": elapsed, "kernel_ms": kern_ms, "split_queries": split_q,
+                              "fallback_queries": fallback_q, "err_ratio": err_ratio}))
         if world > 1:
             dist.destroy_process_group()
         return
@@ -300,9 +306,13 @@ def main():
     if rank == 0:
         n_local = shard.local_rows
         flops = 2.0 * n_local * D_total * a.nq
+        split = split_q > 0
         kname = f"void imgrec::knn_tile_topk_kernel<{tr.value // 128}, {tq.value // 32}"
-        traffic = pmc_traffic(kname) if world == 1 else None
+        traffic = pmc_traffic(kname, split) if world == 1 else None
         achieved = flops / (kern_ms * 1e-3) / 1e12
+        # the split kernel issues 3 bf16 MFMAs per fp32-equivalent product (hi.hi + hi.lo + lo.hi):
+        # its matrix-pipe ceiling for the algorithmic 2NDQ flop is the bf16 dense peak / 3
+        peak = MFMA_BF16_PEAK_TFLOPS / 3 if split else MFMA_F32_PEAK_TFLOPS
         bytes1 = 4.0 * n_local * D_total + 4.0 * n_local
         qps = a.nq * a.steps / elapsed
         out = {
@@ -316,7 +326,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "bf16x3 split (fp32-equivalent) + fp32 rerank" if split else "fp32",
+            "search_mode": a.mode,
+            "split_path": {"queries": split_q, "certificate_fallbacks": fallback_q,
+                           "max_err_over_bound": err_ratio} if split else None,
             "data": "synthetic, generated on device (Gaussian-mixture parts, per-part L2-normalised)",
             "config": {
                 "workload": cfg["name"], "rows": cfg["rows"], "dim": D_total, "k": a.k,
@@ -329,11 +342,14 @@ def main():
             "recall_queries": ngt,
             "max_abs_dist_err_vs_fp64": max_dist_err,
             "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFLOPS,
+                "bound": "mfma", "achieved": achieved, "peak": peak,
+                "unit": "TFLOP/s", "frac": achieved / peak,
+                "peak_basis": ("bf16 dense MFMA 2516.8 TF/s / 3 MFMAs per product" if split
+                               else "fp32 dense MFMA (v_mfma_f32_32x32x2_f32)"),
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
-                "kernel": f"knn_tile_topk_kernel<{tr.value // 128},{tq.value // 32},...>",
+                "kernel": f"knn_tile_topk_kernel<{tr.value // 128},{tq.value // 32},...,"
+                          f"{'true' if split else 'false'}>",
                 "kernel_ms": kern_ms,
                 "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
             },

@@ -108,6 +108,23 @@ Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
 
 constexpr int64_t kQueryChunk = 8192;
 
+// Split-bf16 candidate path (knn_refine.hip): used for batches the (1,4) plan covers, k <= 16,
+// rows padded to 32 floats.  K' = candidates kept per query for the exact rerank.
+inline int split_kc(int k) { return k <= 10 ? 16 : (k <= 16 ? 32 : 0); }
+
+// Relative error-bound coefficients of the certificate (DESIGN.md "Split path"), multiplied by
+// |q| * max|x| in the kernel:
+//   split dot:  3.1 * 2^-16 (dropped lo.lo / residual terms of x = hi + lo + r, |r| <= 2^-16 |x|)
+//               + 1.02 * gamma_n, n = 3 MFMAs x (dp/16) steps x 5 (a 16-term tree inside each),
+//               with unit roundoff 2^-23 (allows truncating accumulation);
+//   rerank dot: 1.02 * gamma_n, n = 4*ceil(dp/256) + 8 fp32 FMAs + butterfly levels, u = 2^-24.
+inline float split_coef(int dp) {
+    return (float)(3.1 * std::ldexp(1.0, -16) + 1.02 * (15.0 * (dp / 16) + 16.0) * std::ldexp(1.0, -23));
+}
+inline float rerank_coef(int dp) {
+    return (float)(1.02 * (4.0 * ((dp + 255) / 256) + 8.0) * std::ldexp(1.0, -24));
+}
+
 }  // namespace
 
 struct knn_index {
@@ -116,13 +133,29 @@ struct knn_index {
     bool trained = true;
     float* xb = nullptr;     // cap x dp
     float* xn = nullptr;     // cap
+    uint32_t* xs = nullptr;  // cap x dp split-bf16 copy (split_ok only)
+    float* xn_max = nullptr; // device scalar, max |x|^2 (refreshed when rows change)
+    bool split_ok = false, xn_max_stale = true;
+    int mode = KNN_SEARCH_AUTO;
+    int64_t last_fallback = 0, last_split_queries = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
     // search workspace
     float* qpad = nullptr; size_t qpad_cap = 0;
     float* qnorm = nullptr; size_t qnorm_cap = 0;
+    size_t xn_max_cap = 0;
     float* cand_d = nullptr; size_t cand_d_cap = 0;
     int64_t* cand_i = nullptr; size_t cand_i_cap = 0;
+    uint32_t* qsplit = nullptr; size_t qsplit_cap = 0;
+    float* cand2_d = nullptr; size_t cand2_d_cap = 0;
+    int64_t* cand2_i = nullptr; size_t cand2_i_cap = 0;
+    int* fail = nullptr; size_t fail_cap = 0;          // [0] = count, [1..] = list
+    float* err_ratio = nullptr; size_t err_ratio_cap = 0;
+    float last_err_ratio = 0.f;
+    float* fb_q = nullptr; size_t fb_q_cap = 0;
+    float* fb_qn = nullptr; size_t fb_qn_cap = 0;
+    float* fb_d = nullptr; size_t fb_d_cap = 0;
+    int64_t* fb_i = nullptr; size_t fb_i_cap = 0;
     // host-path staging
     float* hq = nullptr; size_t hq_cap = 0;
     float* hd = nullptr; size_t hd_cap = 0;
@@ -146,6 +179,16 @@ int reserve_rows(knn_index* ix, int64_t need) {
         (void)hipFree(nxb);
         KNN_FAIL(KNN_ENOMEM, "hipMalloc of %lld row norms failed", (long long)ncap);
     }
+    uint32_t* nxs = nullptr;
+    if (ix->split_ok) {
+        e = hipMalloc((void**)&nxs, (size_t)ncap * ix->dp * sizeof(uint32_t));
+        if (e != hipSuccess) {
+            (void)hipFree(nxb);
+            (void)hipFree(nxn);
+            KNN_FAIL(KNN_ENOMEM, "hipMalloc of the %lld-row split copy failed", (long long)ncap);
+        }
+        KNN_HIP(hipMemsetAsync(nxs, 0, (size_t)ncap * ix->dp * sizeof(uint32_t), ix->stream));
+    }
     KNN_HIP(hipMemsetAsync(nxb, 0, (size_t)ncap * ix->dp * sizeof(float), ix->stream));
     KNN_HIP(hipMemsetAsync(nxn, 0, (size_t)ncap * sizeof(float), ix->stream));
     if (ix->ntotal > 0) {
@@ -153,12 +196,17 @@ int reserve_rows(knn_index* ix, int64_t need) {
                                hipMemcpyDeviceToDevice, ix->stream));
         KNN_HIP(hipMemcpyAsync(nxn, ix->xn, (size_t)ix->ntotal * sizeof(float),
                                hipMemcpyDeviceToDevice, ix->stream));
+        if (nxs)
+            KNN_HIP(hipMemcpyAsync(nxs, ix->xs, (size_t)ix->ntotal * ix->dp * sizeof(uint32_t),
+                                   hipMemcpyDeviceToDevice, ix->stream));
     }
     KNN_HIP(hipStreamSynchronize(ix->stream));
     if (ix->xb) (void)hipFree(ix->xb);
     if (ix->xn) (void)hipFree(ix->xn);
+    if (ix->xs) (void)hipFree(ix->xs);
     ix->xb = nxb;
     ix->xn = nxn;
+    ix->xs = nxs;
     ix->cap = ncap;
     return KNN_OK;
 }
@@ -170,49 +218,151 @@ hipStream_t pick(knn_index* ix, void* s) {
     return (hipStream_t)s;
 }
 
+// Timing events around the dominant (fused) kernel launch of a chunk.
+int timed_begin(knn_index* ix, hipStream_t st, hipEvent_t* e1) {
+    *e1 = nullptr;
+    if (!ix->timing) return KNN_OK;
+    if (ix->ev_used + 2 > ix->ev.size()) {
+        for (int i = 0; i < 64; ++i) {
+            hipEvent_t e;
+            KNN_HIP(hipEventCreate(&e));
+            ix->ev.push_back(e);
+        }
+    }
+    KNN_HIP(hipEventRecord(ix->ev[ix->ev_used], st));
+    *e1 = ix->ev[ix->ev_used + 1];
+    ix->ev_used += 2;
+    return KNN_OK;
+}
+
+// Exact fp32 path over nq padded queries (qpad holds make_plan(nq).nq_pad zero-padded rows).
+int exact_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+                int64_t* I, hipStream_t st, bool timed) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const Plan p = make_plan(ix->ntotal, nq, k, ix->cus);
+    int rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    TileArgs a{};
+    a.wr = p.wr; a.wq = p.wq; a.km = p.km;
+    a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
+    a.qp = qpad; a.qnorm = qnorm; a.nq = (int)nq; a.metric = kmetric;
+    a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
+    a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.split = false;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_tile_topk(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    KNN_HIP(imgrec::launch_merge(ix->cand_d, ix->cand_i, nq, p.ncand / p.km, p.km, p.ncand, p.km, k,
+                                 kmetric, 0, D, I, st));
+    return KNN_OK;
+}
+
+bool use_split(const knn_index* ix, int64_t nq, int k) {
+    if (!ix->split_ok || ix->mode == KNN_SEARCH_EXACT || split_kc(k) == 0) return false;
+    if (ix->mode == KNN_SEARCH_SPLIT) return true;
+    // auto: batches the (1,4) plan covers, corpora with enough rows to amortise the rerank
+    return nq > 128 && ix->ntotal >= 16384;
+}
+
+// Split-bf16 candidates + exact rerank + certificate; uncertified queries re-run exactly.
+int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+                int64_t* I, hipStream_t st, bool timed) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const int kc = split_kc(k);
+    Plan p = make_plan(ix->ntotal, nq, kc, ix->cus);
+    if (!(p.wr == 1 && (p.wq == 4 || p.wq == 8))) {      // split tiles exist for (1,4) / (1,8)
+        p = make_plan(ix->ntotal, std::max<int64_t>(nq, 129), kc, ix->cus);
+        p.nqb = (int)((nq + p.bq - 1) / p.bq);
+        p.nq_pad = p.nqb * p.bq;
+        p.wgs = p.nqb * p.nsplit;
+    }
+    int rc;
+    if (ix->xn_max_stale) {
+        if ((rc = grow(&ix->xn_max, &ix->xn_max_cap, 1)) != KNN_OK) return rc;
+        KNN_HIP(imgrec::launch_max_norm(ix->xn, ix->ntotal, ix->xn_max, st));
+        ix->xn_max_stale = false;
+    }
+    if ((rc = grow(&ix->qsplit, &ix->qsplit_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 1)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->err_ratio, &ix->err_ratio_cap, 1)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_split_rows(qpad, p.nq_pad, ix->dp, ix->qsplit, st));
+    TileArgs a{};
+    a.wr = p.wr; a.wq = p.wq; a.km = kc;
+    a.xb = reinterpret_cast<const float*>(ix->xs); a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
+    a.dp = ix->dp; a.qp = reinterpret_cast<const float*>(ix->qsplit); a.qnorm = qnorm;
+    a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
+    a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i;
+    a.ncand = p.nsplit * p.wr * 2 * kc; a.split = true;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_tile_topk(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    // global top-K' approximate candidates, raw ascending keys (merge in its L2 convention)
+    KNN_HIP(imgrec::launch_merge(ix->cand_d, ix->cand_i, nq, a.ncand / kc, kc, a.ncand, kc, kc, 1,
+                                 0, ix->cand2_d, ix->cand2_i, st));
+    KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
+    KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
+    imgrec::RerankArgs r{};
+    r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
+    r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
+    r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = split_coef(ix->dp);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I; r.fail_count = ix->fail;
+    r.fail_list = ix->fail + 1;
+    r.err_ratio = ix->err_ratio;
+    KNN_HIP(imgrec::launch_rerank_certify(r, st));
+    int nfail = 0;
+    float ratio = 0.f;
+    KNN_HIP(hipMemcpyAsync(&nfail, ix->fail, sizeof(int), hipMemcpyDeviceToHost, st));
+    KNN_HIP(hipMemcpyAsync(&ratio, ix->err_ratio, sizeof(float), hipMemcpyDeviceToHost, st));
+    KNN_HIP(hipStreamSynchronize(st));
+    ix->last_err_ratio = std::max(ix->last_err_ratio, ratio);
+    ix->last_split_queries += nq;
+    if (nfail <= 0) return KNN_OK;
+    ix->last_fallback += nfail;
+    const Plan pf = make_plan(ix->ntotal, nfail, k, ix->cus);
+    if ((rc = grow(&ix->fb_q, &ix->fb_q_cap, (size_t)pf.nq_pad * ix->dp)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fb_qn, &ix->fb_qn_cap, (size_t)pf.nq_pad)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fb_d, &ix->fb_d_cap, (size_t)nfail * k)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fb_i, &ix->fb_i_cap, (size_t)nfail * k)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_gather_rows(qpad, qnorm, ix->dp, ix->fail + 1, nfail, pf.nq_pad, ix->fb_q,
+                                       ix->fb_qn, st));
+    if ((rc = exact_chunk(ix, ix->fb_q, ix->fb_qn, nfail, k, ix->fb_d, ix->fb_i, st, false)) != KNN_OK)
+        return rc;
+    KNN_HIP(imgrec::launch_scatter_results(ix->fb_d, ix->fb_i, ix->fail + 1, nfail, k, D, I, st));
+    return KNN_OK;
+}
+
 int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                   hipStream_t st) {
     const int normalize = ix->metric == KNN_METRIC_COSINE;
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    ix->last_fallback = 0;
+    ix->last_split_queries = 0;
+    ix->last_err_ratio = 0.f;
     if (ix->ntotal == 0) {
         KNN_HIP(imgrec::launch_fill_empty(D, I, nq * (int64_t)k, kmetric, st));
         return KNN_OK;
     }
     for (int64_t c0 = 0; c0 < nq; c0 += kQueryChunk) {
         const int64_t cn = std::min(kQueryChunk, nq - c0);
-        const Plan p = make_plan(ix->ntotal, cn, k, ix->cus);
+        const bool split = use_split(ix, cn, k);
+        // padding: both paths tile queries by the plan of this chunk (the split path never by
+        // fewer than 128 queries)
+        const Plan p = make_plan(ix->ntotal, split ? std::max<int64_t>(cn, 129) : cn, k, ix->cus);
+        const int64_t nq_pad = (cn + p.bq - 1) / p.bq * p.bq;
         int rc;
-        if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)p.nq_pad)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)cn * p.ncand)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)cn * p.ncand)) != KNN_OK) return rc;
-        KNN_HIP(imgrec::launch_rows_ingest(q + c0 * ix->d, cn, ix->d, ix->dp, p.nq_pad, normalize,
+        if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;
+        KNN_HIP(imgrec::launch_rows_ingest(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
                                            ix->qpad, ix->qnorm, st));
-        TileArgs a{};
-        a.wr = p.wr; a.wq = p.wq; a.km = p.km;
-        a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
-        a.qp = ix->qpad; a.qnorm = ix->qnorm; a.nq = (int)cn; a.metric = kmetric;
-        a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
-        a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (ix->timing) {
-            if (ix->ev_used + 2 > ix->ev.size()) {
-                for (int i = 0; i < 64; ++i) {
-                    hipEvent_t e;
-                    KNN_HIP(hipEventCreate(&e));
-                    ix->ev.push_back(e);
-                }
-            }
-            e0 = ix->ev[ix->ev_used];
-            e1 = ix->ev[ix->ev_used + 1];
-            ix->ev_used += 2;
-            KNN_HIP(hipEventRecord(e0, st));
-        }
-        KNN_HIP(imgrec::launch_tile_topk(a, st));
-        if (e1) KNN_HIP(hipEventRecord(e1, st));
-        const int nlists = p.ncand / p.km;
-        KNN_HIP(imgrec::launch_merge(ix->cand_d, ix->cand_i, cn, nlists, p.km, p.ncand, p.km, k,
-                                     kmetric, 0, D + c0 * k, I + c0 * k, st));
+        rc = split ? split_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true)
+                   : exact_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true);
+        if (rc != KNN_OK) return rc;
     }
     return KNN_OK;
 }
@@ -225,7 +375,11 @@ int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st) 
     KNN_HIP(imgrec::launch_rows_ingest(x, n, ix->d, ix->dp, n,
                                        ix->metric == KNN_METRIC_COSINE ? 1 : 0,
                                        ix->xb + (size_t)ix->ntotal * ix->dp, ix->xn + ix->ntotal, st));
+    if (ix->split_ok)
+        KNN_HIP(imgrec::launch_split_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp,
+                                          ix->xs + (size_t)ix->ntotal * ix->dp, st));
     ix->ntotal += n;
+    ix->xn_max_stale = true;
     return KNN_OK;
 }
 
@@ -254,6 +408,7 @@ int knn_create(int d, int metric, int device, knn_index_t** out) {
     ix->dp = (int)round_up(d, d >= 512 ? 2 * imgrec::kDepthPad : imgrec::kDepthPad);
     ix->metric = metric;
     ix->device = device;
+    ix->split_ok = ix->dp % 32 == 0 && d >= 256;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
@@ -270,9 +425,11 @@ int knn_free(knn_index_t* ix) {
     if (!ix) return KNN_OK;
     DeviceGuard g(ix->device);
     (void)hipStreamSynchronize(ix->stream);
-    for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->qpad, (void*)ix->qnorm,
-                    (void*)ix->cand_d, (void*)ix->cand_i, (void*)ix->hq, (void*)ix->hd,
-                    (void*)ix->hi})
+    for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
+                    (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,
+                    (void*)ix->qsplit, (void*)ix->cand2_d, (void*)ix->cand2_i, (void*)ix->fail, (void*)ix->err_ratio,
+                    (void*)ix->fb_q, (void*)ix->fb_qn, (void*)ix->fb_d, (void*)ix->fb_i,
+                    (void*)ix->hq, (void*)ix->hd, (void*)ix->hi})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : ix->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ix->stream);
@@ -339,6 +496,7 @@ int knn_reset(knn_index_t* ix) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
     std::lock_guard<std::mutex> lk(ix->mu);
     ix->ntotal = 0;
+    ix->xn_max_stale = true;
     return KNN_OK;
 }
 
@@ -441,6 +599,27 @@ int knn_kernel_time(knn_index_t* ix, double* total_ms, int* launches) {
     *total_ms = tot;
     *launches = (int)(ix->ev_used / 2);
     ix->ev_used = 0;
+    return KNN_OK;
+}
+
+int knn_set_search_mode(knn_index_t* ix, int mode) {
+    if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
+    if (mode != KNN_SEARCH_AUTO && mode != KNN_SEARCH_EXACT && mode != KNN_SEARCH_SPLIT)
+        KNN_FAIL(KNN_EINVAL, "unknown search mode %d", mode);
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (mode == KNN_SEARCH_SPLIT && !ix->split_ok)
+        KNN_FAIL(KNN_EINVAL, "split search needs d >= 256 (rows padded to 32 floats); d = %d", ix->d);
+    ix->mode = mode;
+    return KNN_OK;
+}
+
+int knn_search_stats(knn_index_t* ix, int64_t* split_queries, int64_t* fallback_queries,
+                     float* max_err_ratio) {
+    if (!ix || !split_queries || !fallback_queries) KNN_FAIL(KNN_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(ix->mu);
+    *split_queries = ix->last_split_queries;
+    *fallback_queries = ix->last_fallback;
+    if (max_err_ratio) *max_err_ratio = ix->last_err_ratio;
     return KNN_OK;
 }
 

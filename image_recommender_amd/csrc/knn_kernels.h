@@ -22,6 +22,29 @@ struct TileArgs {
     float* cand_d;              // nq x ncand keys
     int64_t* cand_i;            // nq x ncand labels
     int ncand;
+    bool split;                 // xb / qp hold the split-bf16 layout (knn_refine.hip)
+};
+
+// One rerank + certificate launch over merged split-path candidates (knn_refine.hip).
+struct RerankArgs {
+    const float* qp;            // fp32 padded queries, nq x dp
+    const float* qnorm;
+    int dp;
+    const float* xb;            // fp32 corpus
+    const float* xn;
+    const float* xn_max;        // device scalar: max stored |x|^2
+    int64_t id_offset;
+    const float* cd;            // nq x kc approximate keys, ascending
+    const int64_t* ci;          // nq x kc labels (id_offset applied), -1 = empty
+    int kc;
+    int64_t nq;
+    int k, metric;              // metric 1 = L2, otherwise inner product
+    float c_split, c_fp;        // relative error-bound coefficients (see knn_capi.cpp)
+    float* D;
+    int64_t* I;
+    int* fail_count;            // device counter (zeroed by the caller)
+    int* fail_list;             // nq entries
+    float* err_ratio;           // device max of observed error / bound (>= 0 floats, atomicMax)
 };
 
 constexpr int kTileRowsMax = 256;   // corpus capacity is rounded to this many rows
@@ -34,5 +57,13 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st);
 hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStream_t st);
+
+hipError_t launch_split_rows(const float* src, int64_t n, int dp, uint32_t* dst, hipStream_t st);
+hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st);
+hipError_t launch_gather_rows(const float* src, const float* src_norm, int dp, const int* list,
+                              int64_t n, int64_t n_pad, float* dst, float* dst_norm, hipStream_t st);
+hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int* list, int64_t n,
+                                  int k, float* D, int64_t* I, hipStream_t st);
+hipError_t launch_max_norm(const float* xn, int64_t n, float* out, hipStream_t st);
 
 }  // namespace imgrec

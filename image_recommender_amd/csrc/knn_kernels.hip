@@ -32,6 +32,15 @@
 namespace imgrec {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// 16-B fragment chunk c of a per-lane float array, reinterpreted as 8 bf16 (split layout)
+template <int N>
+__device__ __forceinline__ bf16x8 frag_bf16(const float (&v)[N], int c) {
+    const f32x4 f = {v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+    return __builtin_bit_cast(bf16x8, f);
+}
 
 // ---------------------------------------------------------------------------------------------
 // helpers
@@ -189,8 +198,14 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
     ki[0] = here0 ? id : ki[0];
 }
 
-template <int WR, int WQ, int KM, int NS, int BK>
-__global__ void __launch_bounds__(WR * WQ * 64)
+// 4-wave workgroups run two per CU (two waves per SIMD): hold them to 256 VGPR+AGPR per lane.
+#ifdef IMGREC_ABLATE_NO_WAVES_HINT
+#define IMGREC_MIN_WAVES(nw) 1
+#else
+#define IMGREC_MIN_WAVES(nw) ((nw) == 4 ? 2 : 1)
+#endif
+template <int WR, int WQ, int KM, int NS, int BK, bool SPLIT>
+__global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
                      int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
                      int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
@@ -334,11 +349,29 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #ifndef IMGREC_ABLATE_NO_DMA
             issue_next();                            // refills the buffer the previous stage used
 #endif
+            if constexpr (SPLIT) {
+                // split layout: this lane half's chunks 2s / 2s+1 are the hi / lo bf16 planes of
+                // MFMA k-step s; dot ~= hi.hi + hi.lo + lo.hi (the lo.lo term is below the bound)
 #pragma unroll
-            for (int kk = 0; kk < KH; ++kk) {
+                for (int s2 = 0; s2 < CPR / 4; ++s2) {
+                    const bf16x8 bh = frag_bf16(bq, 2 * s2), bl = frag_bf16(bq, 2 * s2 + 1);
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
+                    for (int b = 0; b < 4; ++b)
+                        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], 2 * s2), bh, acc[b], 0, 0, 0);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], 2 * s2), bl, acc[b], 0, 0, 0);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], 2 * s2 + 1), bh, acc[b], 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < KH; ++kk) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
+                }
             }
         }
 
@@ -541,11 +574,11 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
     return hipGetLastError();
 }
 
-template <int WR, int WQ, int NS, int BK>
+template <int WR, int WQ, int NS, int BK, bool SPLIT = false>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
-    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK>), grid, block, 0, st, a.xb,     \
+    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, SPLIT>), grid, block, 0, st, a.xb, \
                        a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
                        a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
     switch (km) {
@@ -567,6 +600,13 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
 #endif
 
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
+    if (a.split) {
+        // split-bf16 candidate pass (knn_refine.hip certifies and reranks its output)
+        if (a.dp % 32 != 0 || (a.km != 16 && a.km != 32)) return hipErrorInvalidValue;
+        if (a.wr == 1 && a.wq == 4) return launch_tile_km<1, 4, 2, 32, true>(a.km, a, st);
+        if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, 3, 32, true>(a.km, a, st);
+        return hipErrorInvalidValue;
+    }
     if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)
         return launch_tile_km<1, 8, 4, 16>(a.km, a, st);
     if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, IMGREC_NS_BIG, IMGREC_BK_BIG>(a.km, a, st);

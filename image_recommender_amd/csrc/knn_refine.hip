@@ -1,0 +1,264 @@
+// knn_refine.hip — split-bf16 candidate path of the exact k-NN search (gfx950).
+//
+// The fused kernel (knn_kernels.hip, SPLIT=true) scores every corpus row against every query with
+// three bf16 MFMAs per 16-deep step (x = hi + lo, both bf16; q.x ~= qh.xh + qh.xl + ql.xh), 5.3x
+// fewer matrix cycles than the exact v_mfma_f32_32x32x2_f32 form, and keeps the K' best
+// approximate keys per query (K' > k).  This file turns that candidate set into the exact answer:
+//
+//   split_rows      fp32 rows -> split layout (per 32-deep stage, per lane half h and MFMA k-step
+//                   s: a 16-B hi chunk and a 16-B lo chunk holding depth 32j + 16s + 8h + 0..7).
+//   rerank_certify  one wave per query: exact fp32 keys of the K' candidates (the same
+//                   faiss exhaustive_L2sqr_blas key form as the exact kernel), top-k by
+//                   (key, label), and a certificate that no row outside the candidate set can
+//                   rank before a returned row:
+//                       tau - E_approx > s_k + E_fp32
+//                   tau = K'-th approximate key (every excluded row's approximate key is >= tau),
+//                   s_k = k-th exact key, E_* rigorous error bounds (DESIGN.md "Split path").
+//                   A query whose certificate fails is listed; the host re-runs it on the exact
+//                   fp32 kernel.  So the returned (D, I) always carry the exact path's guarantee.
+//   gather_rows / scatter_results   compact the failed queries for that re-run and put back.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <float.h>
+#include <math.h>
+
+#include <algorithm>
+
+#include "knn_kernels.h"
+
+namespace imgrec {
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// one thread per (row, 32-deep stage j, lane half h, k-step s): 8 floats in, 32 B out
+__global__ void __launch_bounds__(256)
+split_rows_kernel(const float* __restrict__ src, int64_t n, int dp, uint32_t* __restrict__ dst) {
+    const int per_row = dp / 8;                      // (dp/32) stages x 4 (h, s) pairs
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * per_row) return;
+    const int64_t row = t / per_row;
+    const int r = (int)(t - row * per_row);
+    const int j = r >> 2, h = (r >> 1) & 1, s = r & 1;
+    const float* x = src + row * dp + j * 32 + 16 * s + 8 * h;
+    const float4 v0 = *reinterpret_cast<const float4*>(x);
+    const float4 v1 = *reinterpret_cast<const float4*>(x + 4);
+    const float e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const uint32_t h0 = bf16_rne(e[2 * p]), h1 = bf16_rne(e[2 * p + 1]);
+        const uint32_t l0 = bf16_rne(e[2 * p] - __uint_as_float(h0 << 16));
+        const uint32_t l1 = bf16_rne(e[2 * p + 1] - __uint_as_float(h1 << 16));
+        hi[p] = h0 | (h1 << 16);
+        lo[p] = l0 | (l1 << 16);
+    }
+    // logical chunk h*4 + 2s (hi) and +1 (lo): 32 contiguous bytes
+    uint32_t* o = dst + row * dp + j * 32 + (h * 4 + 2 * s) * 4;
+    *reinterpret_cast<uint4*>(o) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    *reinterpret_cast<uint4*>(o + 4) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+}
+
+template <typename I>
+__device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
+    return d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+// One wave per query.  cd/ci: the merged approximate candidates, nq x kc, ascending raw keys
+// (L2 distance or -ip), empty = label -1.
+__global__ void __launch_bounds__(256)
+rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qnorm, int dp,
+                      const float* __restrict__ xb, const float* __restrict__ xn,
+                      const float* __restrict__ xn_max, int64_t id_offset,
+                      const float* __restrict__ cd, const int64_t* __restrict__ ci, int kc,
+                      int64_t nq, int k, int metric, float c_split, float c_fp,
+                      float* __restrict__ D, int64_t* __restrict__ I, int* __restrict__ fail_count,
+                      int* __restrict__ fail_list, float* __restrict__ err_ratio) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const float* qv = qp + q * dp;
+    const float qn = qnorm[q];
+    const int64_t lab = lane < kc ? ci[q * kc + lane] : (int64_t)-1;
+    float key = INFINITY;
+
+    // exact fp32 keys, four candidates per pass (independent loads in flight)
+    const int n4 = dp / 4;
+    for (int c0 = 0; c0 < kc; c0 += 4) {
+        int64_t rows[4];
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = min(c0 + u, kc - 1);
+            const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
+            const int hi32 = __shfl((int)(lab >> 32), c, 64);
+            const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
+            rows[u] = (c0 + u < kc && l >= 0) ? l - id_offset : (int64_t)-1;
+        }
+        for (int i = lane; i < n4; i += 64) {
+            const float4 a = reinterpret_cast<const float4*>(qv)[i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (rows[u] < 0) continue;
+                const float4 b = reinterpret_cast<const float4*>(xb + rows[u] * dp)[i];
+                acc[u] = fmaf(a.x, b.x, acc[u]);
+                acc[u] = fmaf(a.y, b.y, acc[u]);
+                acc[u] = fmaf(a.z, b.z, acc[u]);
+                acc[u] = fmaf(a.w, b.w, acc[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off, 64);
+            if (rows[u] < 0 || lane != c0 + u) continue;
+            float kv;
+            if (metric == 1) {
+                kv = fmaf(-2.f, acc[u], qn + xn[rows[u]]);
+                kv = kv < 0.f ? 0.f : kv;
+            } else {
+                kv = -acc[u];
+            }
+            key = kv;
+        }
+    }
+
+    // rank of this lane's candidate among the valid ones by (key, label)
+    const bool valid = lab >= 0;
+    int rank = 0, nvalid = 0;
+    for (int i = 0; i < kc; ++i) {
+        const float ok = __shfl(key, i, 64);
+        const int lo32 = __shfl((int)(lab & 0xffffffff), i, 64);
+        const int hi32 = __shfl((int)(lab >> 32), i, 64);
+        const int64_t ol = ((int64_t)hi32 << 32) | (uint32_t)lo32;
+        if (ol < 0) continue;
+        ++nvalid;
+        if (valid && ranks_before_r(ok, ol, key, lab)) ++rank;
+    }
+    if (valid && rank < k) {
+        D[q * k + rank] = (metric == 1) ? key : -key;
+        I[q * k + rank] = lab;
+    }
+    if (lane >= nvalid && lane < k) {
+        D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
+        I[q * k + lane] = -1;
+    }
+
+    const float xm = *xn_max;
+    const float nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
+    const float u = 1.0f / 8388608.f;               // 2^-23
+    auto bound_a = [&](float v) {                   // |approx key - exact key| bound at key v
+        return metric == 1 ? 2.f * c_split * nn + 2.f * u * (qn + xm + fabsf(v)) : c_split * nn;
+    };
+    auto bound_f = [&](float v) {                   // |fp32 rerank key - exact key| bound
+        return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
+    };
+
+    // observed |approx - rerank| of every candidate relative to the two bounds (<= 1 whenever
+    // the bounds hold; reported by knn_search_stats so tests and the bench can watch it)
+    if (valid) {
+        const float ak = cd[q * kc + lane];
+        const float r = fabsf(ak - key) / (bound_a(ak) + bound_f(key));
+        atomicMax(reinterpret_cast<unsigned*>(err_ratio), __float_as_uint(r));
+    }
+
+    // certificate (a full candidate set only: fewer than kc candidates means every row is one)
+    const int64_t lab_tau = ci[q * kc + kc - 1];
+    if (lab_tau < 0 || nvalid < kc) return;
+    const float tau = cd[q * kc + kc - 1];
+    float sk = (valid && rank == k - 1) ? key : -INFINITY;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
+    const bool certified = (tau - bound_a(tau)) > (sk + bound_f(sk));
+    if (!certified && lane == 0) fail_list[atomicAdd(fail_count, 1)] = (int)q;
+}
+
+__global__ void __launch_bounds__(256)
+gather_rows_kernel(const float* __restrict__ src, const float* __restrict__ src_norm, int dp,
+                   const int* __restrict__ list, int64_t n, int64_t n_pad,
+                   float* __restrict__ dst, float* __restrict__ dst_norm) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n_pad) return;
+    float* o = dst + row * dp;
+    if (row >= n) {
+        for (int j = lane; j < dp; j += 64) o[j] = 0.f;
+        if (lane == 0) dst_norm[row] = 0.f;
+        return;
+    }
+    const float* s = src + (int64_t)list[row] * dp;
+    for (int j = lane; j < dp; j += 64) o[j] = s[j];
+    if (lane == 0) dst_norm[row] = src_norm[list[row]];
+}
+
+__global__ void __launch_bounds__(256)
+scatter_results_kernel(const float* __restrict__ sd, const int64_t* __restrict__ si,
+                       const int* __restrict__ list, int64_t n, int k, float* __restrict__ D,
+                       int64_t* __restrict__ I) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * k) return;
+    const int64_t r = t / k;
+    const int j = (int)(t - r * k);
+    D[(int64_t)list[r] * k + j] = sd[t];
+    I[(int64_t)list[r] * k + j] = si[t];
+}
+
+__global__ void max_norm_kernel(const float* __restrict__ xn, int64_t n, float* __restrict__ out) {
+    float m = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, xn[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    // norms are >= 0: their IEEE bit patterns order like unsigned integers
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(m));
+}
+
+// ---------------------------------------------------------------------------------------------
+hipError_t launch_split_rows(const float* src, int64_t n, int dp, uint32_t* dst, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (dp % 32 != 0) return hipErrorInvalidValue;
+    const int64_t threads = n * (dp / 8);
+    hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
+                       src, n, dp, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
+    if (a.nq <= 0) return hipSuccess;
+    if (a.kc > 64 || a.k > a.kc || a.dp % 4 != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rerank_certify_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, st,
+                       a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci, a.kc,
+                       a.nq, a.k, a.metric, a.c_split, a.c_fp, a.D, a.I, a.fail_count, a.fail_list,
+                       a.err_ratio);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const float* src, const float* src_norm, int dp, const int* list,
+                              int64_t n, int64_t n_pad, float* dst, float* dst_norm, hipStream_t st) {
+    if (n_pad <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n_pad + 3) / 4)), dim3(256), 0, st, src,
+                       src_norm, dp, list, n, n_pad, dst, dst_norm);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int* list, int64_t n,
+                                  int k, float* D, int64_t* I, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((n * k + 255) / 256)), dim3(256), 0,
+                       st, sd, si, list, n, k, D, I);
+    return hipGetLastError();
+}
+
+hipError_t launch_max_norm(const float* xn, int64_t n, float* out, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float), st);
+    if (e != hipSuccess || n <= 0) return e;
+    const int64_t blocks = std::min<int64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(max_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, st, xn, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace imgrec

@@ -168,6 +168,30 @@ class Index:
     def reserve(self, n: int) -> None:
         _lib.check(_lib.load().knn_reserve(self._h, int(n)), "knn_reserve")
 
+    # -- search arithmetic (extension; include/imgrec_knn.h knn_search_mode) -------------------
+    SEARCH_MODES = {"auto": _lib.KNN_SEARCH_AUTO, "exact": _lib.KNN_SEARCH_EXACT,
+                    "split": _lib.KNN_SEARCH_SPLIT}
+
+    @property
+    def search_mode(self) -> str:
+        return getattr(self, "_mode", "auto")
+
+    @search_mode.setter
+    def search_mode(self, mode: str) -> None:
+        if mode not in self.SEARCH_MODES:
+            raise ValueError(f"search_mode must be one of {sorted(self.SEARCH_MODES)}")
+        _lib.check(_lib.load().knn_set_search_mode(self._h, self.SEARCH_MODES[mode]),
+                   "knn_set_search_mode")
+        self._mode = mode
+
+    def search_stats(self, with_error: bool = False):
+        """(queries of the last search on the split path, of which re-run on the exact kernel)
+        [+ largest observed approximation error / certificate bound, with_error=True]."""
+        a, b, r = C.c_int64(), C.c_int64(), C.c_float()
+        _lib.check(_lib.load().knn_search_stats(self._h, C.byref(a), C.byref(b), C.byref(r)),
+                   "knn_search_stats")
+        return (a.value, b.value, r.value) if with_error else (a.value, b.value)
+
 
 class IndexFlat(Index):
     def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1):

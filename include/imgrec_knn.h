@@ -58,6 +58,19 @@ enum knn_error {
     KNN_ENOSYS = -5    /* not supported (e.g. no GPU visible) */
 };
 
+/* Search arithmetic.  AUTO: batches of > 128 queries with k <= 16 on an index with d >= 256 take
+ * the split path (bf16 hi/lo candidate pass, exact fp32 rerank of K' candidates and a per-query
+ * error-bound certificate; uncertified queries re-run on the exact kernel), everything else the
+ * exact fp32 kernel.  Both return the same results up to fp32 rounding of the distances: the
+ * certificate guarantees the candidate set contains every row the exact search could return.
+ * EXACT: always the fp32 kernel.  SPLIT: the split path whenever k <= 16 (tests).
+ * A split-path search synchronises its stream once per 8192-query chunk (certificate count). */
+enum knn_search_mode {
+    KNN_SEARCH_AUTO = 0,
+    KNN_SEARCH_EXACT = 1,
+    KNN_SEARCH_SPLIT = 2
+};
+
 /* Largest k one search can return (the fused top-k keeps per-lane lists of this length). */
 #define KNN_MAX_K 32
 
@@ -111,6 +124,14 @@ int knn_normalize_L2(float* x_host, int64_t n, int d);
  * count since the last call, and clears them. */
 int knn_set_timing(knn_index_t* index, int enable);
 int knn_kernel_time(knn_index_t* index, double* total_ms, int* launches);
+
+int knn_set_search_mode(knn_index_t* index, int mode);
+/* Queries of the last search that took the split path, how many of them failed the certificate
+ * and were re-run on the exact kernel, and (may be NULL) the largest observed
+ * |approximate key - fp32 key| / (error bound of both) over all candidates: <= 1 whenever the
+ * certificate's bounds hold, in practice far below. */
+int knn_search_stats(knn_index_t* index, int64_t* split_queries, int64_t* fallback_queries,
+                     float* max_err_ratio);
 
 /* Launch geometry chosen for a search of nq queries (for reports): workgroup tile rows/queries,
  * row splits and workgroup count. */
