@@ -108,6 +108,34 @@ Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
 
 constexpr int64_t kQueryChunk = 8192;
 
+#ifndef IMGREC_SPLIT_WR
+#define IMGREC_SPLIT_WR 1
+#endif
+#ifndef IMGREC_SPLIT_WQ
+#define IMGREC_SPLIT_WQ 4
+#endif
+#ifndef IMGREC_SPLIT_WGPCU
+#define IMGREC_SPLIT_WGPCU 2
+#endif
+
+// Split-path geometry: one tile shape for every batch size.
+Plan make_split_plan(int64_t ntotal, int64_t nq, int kc, int cus) {
+    Plan p{};
+    p.km = kc;
+    p.wr = IMGREC_SPLIT_WR;
+    p.wq = IMGREC_SPLIT_WQ;
+    p.bm = p.wr * 128;
+    p.bq = p.wq * 32;
+    p.nqb = (int)((nq + p.bq - 1) / p.bq);
+    p.nq_pad = p.nqb * p.bq;
+    p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+    const int target = cus * IMGREC_SPLIT_WGPCU;
+    p.nsplit = std::max(1, std::min((target + p.nqb - 1) / p.nqb, p.ntiles));
+    p.ncand = p.nsplit * p.wr * 2 * p.km;
+    p.wgs = p.nqb * p.nsplit;
+    return p;
+}
+
 // Split-bf16 candidate path (knn_refine.hip): used for batches the (1,4) plan covers, k <= 16,
 // rows padded to 32 floats.  K' = candidates kept per query for the exact rerank.
 inline int split_kc(int k) { return k <= 10 ? 16 : (k <= 16 ? 32 : 0); }
@@ -270,13 +298,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
                 int64_t* I, hipStream_t st, bool timed) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = split_kc(k);
-    Plan p = make_plan(ix->ntotal, nq, kc, ix->cus);
-    if (!(p.wr == 1 && (p.wq == 4 || p.wq == 8))) {      // split tiles exist for (1,4) / (1,8)
-        p = make_plan(ix->ntotal, std::max<int64_t>(nq, 129), kc, ix->cus);
-        p.nqb = (int)((nq + p.bq - 1) / p.bq);
-        p.nq_pad = p.nqb * p.bq;
-        p.wgs = p.nqb * p.nsplit;
-    }
+    const Plan p = make_split_plan(ix->ntotal, nq, kc, ix->cus);
     int rc;
     if (ix->xn_max_stale) {
         if ((rc = grow(&ix->xn_max, &ix->xn_max_cap, 1)) != KNN_OK) return rc;
@@ -351,10 +373,10 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     for (int64_t c0 = 0; c0 < nq; c0 += kQueryChunk) {
         const int64_t cn = std::min(kQueryChunk, nq - c0);
         const bool split = use_split(ix, cn, k);
-        // padding: both paths tile queries by the plan of this chunk (the split path never by
-        // fewer than 128 queries)
-        const Plan p = make_plan(ix->ntotal, split ? std::max<int64_t>(cn, 129) : cn, k, ix->cus);
-        const int64_t nq_pad = (cn + p.bq - 1) / p.bq * p.bq;
+        // padding: the query tile of the plan this chunk will run
+        const Plan p = split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
+                             : make_plan(ix->ntotal, cn, k, ix->cus);
+        const int64_t nq_pad = p.nq_pad;
         int rc;
         if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;

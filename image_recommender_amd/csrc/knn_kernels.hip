@@ -137,7 +137,9 @@ struct TileGeom {
     static constexpr int SA = BM * BK, SB = BQ * BK, STAGE = SA + SB;   // floats
     static constexpr int PA = BM / RPP, PB = BQ / RPP, PIECES = PA + PB;
     static constexpr int LPW = PIECES / NW;            // pieces per wave per stage
-    static constexpr int PARK = NW * 8 * 64;           // epilogue key parking (in a spent stage)
+    // epilogue key parking in a spent stage: all 16 keys of a block in one round when they fit
+    static constexpr int PR = (SA + SB) >= NW * 16 * 64 ? 16 : 8;
+    static constexpr int PARK = NW * PR * 64;
     static constexpr int LDS_FLOATS = NS * STAGE + NS * BM;
     static_assert(BK == 16 || BK == 32, "stage depth");
     static_assert(PIECES % NW == 0, "pieces must divide evenly over waves");
@@ -212,7 +214,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                      float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand) {
     using G = TileGeom<WR, WQ, NS, BK>;
     constexpr int NW = G::NW, BM = G::BM, BQ = G::BQ, SA = G::SA, STAGE = G::STAGE;
-    constexpr int PA = G::PA, LPW = G::LPW, CPR = G::CPR, RPP = G::RPP, RPB = G::RPB;
+    constexpr int PA = G::PA, LPW = G::LPW, CPR = G::CPR, RPP = G::RPP, RPB = G::RPB, PR = G::PR;
     constexpr int KH = BK / 2;          // MFMA sub-steps per stage (each covers depth 2)
 
     __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
@@ -390,41 +392,50 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
         if (qvalid) {
 #endif
             const float* nrm = norm_base + ((t - t0) % NS) * BM;
-            float* park = const_cast<float*>(st) + wave * (8 * 64);
+            float* park = const_cast<float*>(st) + wave * (PR * 64);
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 float key[16];
                 unsigned mask = 0;
                 const float tau = kd[KM - 1];
                 const float tau_p = __shfl_xor(tau, 32, 64);
+                const int rb = wr * 128 + b * 32 + 4 * lh;     // row of accumulator reg 0
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int rl = wr * 128 + b * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                    const float ip = acc[b][r];
-                    float kv;
-                    if (metric == 1) {
-                        kv = fmaf(-2.f, ip, qn + nrm[rl]);
-                        kv = kv < 0.f ? 0.f : kv;
-                    } else {
-                        kv = -ip;
+                for (int j = 0; j < 4; ++j) {                  // regs 4j..4j+3 = rows rb+8j+0..3
+                    float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (metric == 1) n4 = *reinterpret_cast<const float4*>(nrm + rb + 8 * j);
+                    const float nv[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * j + i;
+                        const float ip = acc[b][r];
+                        float kv;
+                        if (metric == 1) {
+                            kv = fmaf(-2.f, ip, qn + nv[i]);
+                            kv = kv < 0.f ? 0.f : kv;
+                        } else {
+                            kv = -ip;
+                        }
+                        key[r] = kv;
+                        const bool pass = (row0 + rb + 8 * j + i < nrows) && kv < tau && kv <= tau_p;
+                        mask |= (unsigned)pass << r;
                     }
-                    key[r] = kv;
-                    const bool pass = (row0 + rl < nrows) && kv < tau && kv <= tau_p;
-                    mask |= (unsigned)pass << r;
                 }
-                // two parking rounds of 8 keys (the park must fit in one spent stage)
+                // survivors are inserted one per iteration per lane (ctz walk of the lane's own
+                // mask): the wave loops max-popcount times, not once per row any lane needs
 #pragma unroll
-                for (int h8 = 0; h8 < 2; ++h8) {
-                    const unsigned m8 = (mask >> (8 * h8)) & 0xffu;
-                    if (__any(m8 != 0)) {
+                for (int h = 0; h < 16 / PR; ++h) {
+                    unsigned m = (mask >> (PR * h)) & ((1u << PR) - 1u);
+                    if (__any(m != 0)) {
 #pragma unroll
-                        for (int r = 0; r < 8; ++r) park[r * 64 + lane] = key[8 * h8 + r];
-#pragma unroll 1
-                        for (int r = 0; r < 8; ++r) {
-                            if ((m8 >> r) & 1u) {
+                        for (int r = 0; r < PR; ++r) park[r * 64 + lane] = key[PR * h + r];
+                        while (__any(m != 0)) {
+                            if (m) {
+                                const int r = __builtin_ctz(m);
+                                m &= m - 1u;
                                 const float kv = park[r * 64 + lane];
-                                const int rr8 = 8 * h8 + r;
-                                const int row = row0 + wr * 128 + b * 32 + (rr8 & 3) + 8 * (rr8 >> 2) + 4 * lh;
+                                const int rr = PR * h + r;
+                                const int row = row0 + rb + (rr & 3) + 8 * (rr >> 2);
                                 if (kv < kd[KM - 1]) list_insert_mono<KM>(kd, ki, kv, row);
                             }
                         }
@@ -604,7 +615,10 @@ hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
         // split-bf16 candidate pass (knn_refine.hip certifies and reranks its output)
         if (a.dp % 32 != 0 || (a.km != 16 && a.km != 32)) return hipErrorInvalidValue;
         if (a.wr == 1 && a.wq == 4) return launch_tile_km<1, 4, 2, 32, true>(a.km, a, st);
+#ifdef IMGREC_SPLIT_VARIANTS
         if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, 3, 32, true>(a.km, a, st);
+        if (a.wr == 2 && a.wq == 4) return launch_tile_km<2, 4, 3, 32, true>(a.km, a, st);
+#endif
         return hipErrorInvalidValue;
     }
     if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)

@@ -12,6 +12,6 @@ for rep in 1 2; do
   done
 done
 for v in "$@"; do
-  IMGREC_LIB_NAME=$v timeout -k 10 600 python -m pytest tests/test_knn_gpu.py -x -q -m gpu > $OUT/pytest_$v.log 2>&1 || { echo "$v tests failed"; tail -30 $OUT/pytest_$v.log; exit 2; }
+  IMGREC_LIB_NAME=$v timeout -k 10 600 python -m pytest ${TESTS:-tests/test_knn_gpu.py} -x -q -m gpu > $OUT/pytest_$v.log 2>&1 || { echo "$v tests failed"; tail -30 $OUT/pytest_$v.log; exit 2; }
   echo "$v $(tail -1 $OUT/pytest_$v.log)"
 done

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc CSVs of the fused kernel (per-dispatch averages)."""
 import collections, csv, glob, sys
 out = sys.argv[1]
-for f in sorted(glob.glob(f"{out}/pmc*/run_counter_collection.csv")):
+for f in sorted(glob.glob(f"{out}/*/run_counter_collection.csv")):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
