@@ -108,27 +108,21 @@ Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
 
 constexpr int64_t kQueryChunk = 8192;
 
-#ifndef IMGREC_SPLIT_WR
-#define IMGREC_SPLIT_WR 1
-#endif
-#ifndef IMGREC_SPLIT_WQ
-#define IMGREC_SPLIT_WQ 4
-#endif
-#ifndef IMGREC_SPLIT_WGPCU
-#define IMGREC_SPLIT_WGPCU 2
-#endif
-
-// Split-path geometry: one tile shape for every batch size.
+// Split-path geometry: one tile shape for every batch size ((1,4) workgroups, two per CU,
+// kSplitWB row blocks per wave).
 Plan make_split_plan(int64_t ntotal, int64_t nq, int kc, int cus) {
     Plan p{};
     p.km = kc;
-    p.wr = IMGREC_SPLIT_WR;
-    p.wq = IMGREC_SPLIT_WQ;
-    p.bm = p.wr * 128;
+    p.wr = 1;
+    p.wq = 4;
+    p.bm = p.wr * 32 * imgrec::kSplitWB;
     p.bq = p.wq * 32;
     p.nqb = (int)((nq + p.bq - 1) / p.bq);
     p.nq_pad = p.nqb * p.bq;
     p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+#ifndef IMGREC_SPLIT_WGPCU
+#define IMGREC_SPLIT_WGPCU 2
+#endif
     const int target = cus * IMGREC_SPLIT_WGPCU;
     p.nsplit = std::max(1, std::min((target + p.nqb - 1) / p.nqb, p.ntiles));
     p.ncand = p.nsplit * p.wr * 2 * p.km;
@@ -312,7 +306,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 1)) != KNN_OK) return rc;
     if ((rc = grow(&ix->err_ratio, &ix->err_ratio_cap, 1)) != KNN_OK) return rc;
-    KNN_HIP(imgrec::launch_split_rows(qpad, p.nq_pad, ix->dp, ix->qsplit, st));
+    KNN_HIP(imgrec::launch_split_rows(qpad, p.nq_pad, ix->dp, imgrec::kSplitBK, ix->qsplit, st));
     TileArgs a{};
     a.wr = p.wr; a.wq = p.wq; a.km = kc;
     a.xb = reinterpret_cast<const float*>(ix->xs); a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
@@ -320,6 +314,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
     a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i;
     a.ncand = p.nsplit * p.wr * 2 * kc; a.split = true;
+    a.wb = imgrec::kSplitWB; a.sbk = imgrec::kSplitBK;
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
     KNN_HIP(imgrec::launch_tile_topk(a, st));
@@ -399,7 +394,7 @@ int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st) 
                                        ix->xb + (size_t)ix->ntotal * ix->dp, ix->xn + ix->ntotal, st));
     if (ix->split_ok)
         KNN_HIP(imgrec::launch_split_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp,
-                                          ix->xs + (size_t)ix->ntotal * ix->dp, st));
+                                          imgrec::kSplitBK, ix->xs + (size_t)ix->ntotal * ix->dp, st));
     ix->ntotal += n;
     ix->xn_max_stale = true;
     return KNN_OK;

@@ -10,6 +10,8 @@ namespace imgrec {
 // Arguments of one fused distance + top-k launch.
 struct TileArgs {
     int wr, wq, km;             // waves along rows / queries, register list length
+    int wb = 4;                 // 32-row MFMA blocks per wave (rows per wave = 32*wb)
+    int sbk = 0;                // split path: staging depth the split copy is laid out for
     const float* xb;            // corpus, nrows_cap x dp (rows padded to 256, columns to 16)
     const float* xnorm;         // |x|^2 per stored row
     int nrows, dp;
@@ -50,6 +52,18 @@ struct RerankArgs {
 constexpr int kTileRowsMax = 256;   // corpus capacity is rounded to this many rows
 constexpr int kDepthPad = 16;       // row stride is rounded to this many floats
 
+// Split-path tile: (1,4) workgroups of kSplitWB-block waves, kSplitBK-word stages, kSplitNS ring.
+#ifndef IMGREC_SPLIT_BK
+#define IMGREC_SPLIT_BK 32
+#endif
+#ifndef IMGREC_SPLIT_NS
+#define IMGREC_SPLIT_NS 2
+#endif
+#ifndef IMGREC_SPLIT_WB
+#define IMGREC_SPLIT_WB 4
+#endif
+constexpr int kSplitBK = IMGREC_SPLIT_BK, kSplitNS = IMGREC_SPLIT_NS, kSplitWB = IMGREC_SPLIT_WB;
+
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st);
@@ -58,7 +72,8 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
                         float* D, int64_t* I, hipStream_t st);
 hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStream_t st);
 
-hipError_t launch_split_rows(const float* src, int64_t n, int dp, uint32_t* dst, hipStream_t st);
+hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32_t* dst,
+                             hipStream_t st);
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st);
 hipError_t launch_gather_rows(const float* src, const float* src_norm, int dp, const int* list,
                               int64_t n, int64_t n_pad, float* dst, float* dst_norm, hipStream_t st);

@@ -31,6 +31,16 @@
 
 namespace imgrec {
 
+#ifdef IMGREC_PROF
+// Debug build only: per-phase s_memtime cycle totals of the fused kernel, summed over waves.
+__device__ unsigned long long g_prof[8];
+#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(i, d) prof[i] += (d)
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, d)
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -111,8 +121,8 @@ rows_ingest_kernel(const float* __restrict__ src, int64_t n, int d, int dp, int6
 // ---------------------------------------------------------------------------------------------
 // knn_tile_topk
 //
-// Workgroup = WR x WQ waves; wave tile = 128 corpus rows (4 MFMA row blocks) x 32 queries, so the
-// workgroup tile is BM = 128*WR rows x BQ = 32*WQ queries.  A workgroup owns one query block and a
+// Workgroup = WR x WQ waves; wave tile = 32*WB corpus rows (WB MFMA row blocks, 4 or 8) x 32
+// queries, so the workgroup tile is BM = 32*WB*WR rows x BQ = 32*WQ queries.  A workgroup owns one query block and a
 // contiguous range of row tiles (a "row split") and streams it as one continuous sequence of
 // BK-deep K stages: (tile t0, stage 0..nsteps-1), (t0+1, 0..), ...
 //
@@ -127,10 +137,11 @@ rows_ingest_kernel(const float* __restrict__ src, int64_t n, int d, int dp, int6
 // GLOBAL source address (the DMA destination is lane-linear); the fragment reads apply the same
 // XOR, which makes every ds_read_b128 16-lane group hit 16 distinct 16-B bank slots.
 // ---------------------------------------------------------------------------------------------
-template <int WR, int WQ, int NS, int BK>
+template <int WR, int WQ, int NS, int BK, int WB = 4>
 struct TileGeom {
     static constexpr int NW = WR * WQ, NT = NW * 64;
-    static constexpr int BM = WR * 128, BQ = WQ * 32;
+    static constexpr int RW = 32 * WB;                 // corpus rows per wave
+    static constexpr int BM = WR * RW, BQ = WQ * 32;
     static constexpr int CPR = BK / 4;                 // 16-B chunks per staged row
     static constexpr int RPP = 64 / CPR;               // rows per 1-KiB DMA piece
     static constexpr int RPB = 64 / BK;                // rows per 256-B bank row
@@ -206,13 +217,14 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
 #else
 #define IMGREC_MIN_WAVES(nw) ((nw) == 4 ? 2 : 1)
 #endif
-template <int WR, int WQ, int KM, int NS, int BK, bool SPLIT>
+template <int WR, int WQ, int KM, int NS, int BK, bool SPLIT, int WB>
 __global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
                      int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
                      int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
                      float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand) {
-    using G = TileGeom<WR, WQ, NS, BK>;
+    using G = TileGeom<WR, WQ, NS, BK, WB>;
+    constexpr int RW = G::RW;
     constexpr int NW = G::NW, BM = G::BM, BQ = G::BQ, SA = G::SA, STAGE = G::STAGE;
     constexpr int PA = G::PA, LPW = G::LPW, CPR = G::CPR, RPP = G::RPP, RPB = G::RPB, PR = G::PR;
     constexpr int KH = BK / 2;          // MFMA sub-steps per stage (each covers depth 2)
@@ -305,15 +317,20 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     int remaining = (t1 - t0) * nsteps;     // stages not yet consumed
     int cbuf = 0;
 
+#ifdef IMGREC_PROF
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    PROF_T(tk0);
+#endif
     for (int t = t0; t < t1; ++t) {
         const int row0 = t * BM;
-        f32x16 acc[4];
+        f32x16 acc[WB];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[b] = (f32x16){0.f};
+        for (int b = 0; b < WB; ++b) acc[b] = (f32x16){0.f};
 
         const float* st = smem;
         for (int s = 0; s < nsteps; ++s) {
             // own DMA of this stage landed (later stages may stay in flight)
+            PROF_T(ta);
             --remaining;                             // stages issued after this one: min(NS-2, remaining)
 #ifdef IMGREC_ABLATE_NO_WAIT
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -322,11 +339,13 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
             else if (NS > 3 && remaining == 1) wait_vmcnt<LPW>();
             else wait_vmcnt<0>();
 #endif
+            PROF_T(tb);
             barrier_raw();                           // everyone's DMA landed; previous stage read
+            PROF_T(tc);
 
             st = smem + cbuf * STAGE;
             cbuf = (cbuf + 1 == NS) ? 0 : cbuf + 1;
-            float a[4][KH], bq[KH];
+            float a[WB][KH], bq[KH];
             {
                 const float* bp = st + SA + wq * 32 * BK;
 #pragma unroll
@@ -336,8 +355,8 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                 }
             }
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const float* ap = st + (wr * 128 + b * 32) * BK;
+            for (int b = 0; b < WB; ++b) {
+                const float* ap = st + (wr * RW + b * 32) * BK;
 #pragma unroll
                 for (int c = 0; c < CPR / 2; ++c) {
                     const float4 v = *reinterpret_cast<const float4*>(ap + fo[c]);
@@ -351,6 +370,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #ifndef IMGREC_ABLATE_NO_DMA
             issue_next();                            // refills the buffer the previous stage used
 #endif
+            PROF_T(td);
             if constexpr (SPLIT) {
                 // split layout: this lane half's chunks 2s / 2s+1 are the hi / lo bf16 planes of
                 // MFMA k-step s; dot ~= hi.hi + hi.lo + lo.hi (the lo.lo term is below the bound)
@@ -358,23 +378,27 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                 for (int s2 = 0; s2 < CPR / 4; ++s2) {
                     const bf16x8 bh = frag_bf16(bq, 2 * s2), bl = frag_bf16(bq, 2 * s2 + 1);
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < WB; ++b)
                         acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], 2 * s2), bh, acc[b], 0, 0, 0);
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < WB; ++b)
                         acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], 2 * s2), bl, acc[b], 0, 0, 0);
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < WB; ++b)
                         acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], 2 * s2 + 1), bh, acc[b], 0, 0, 0);
                 }
             } else {
 #pragma unroll
                 for (int kk = 0; kk < KH; ++kk) {
 #pragma unroll
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < WB; ++b)
                         acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
                 }
             }
+#ifdef IMGREC_PROF
+            PROF_T(te);
+            PROF_ADD(0, tb - ta); PROF_ADD(1, tc - tb); PROF_ADD(2, td - tc); PROF_ADD(3, te - td);
+#endif
         }
 
         // ---- epilogue: key = L2 distance (faiss exhaustive_L2sqr_blas form, clamped at 0) or
@@ -384,8 +408,10 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
         // (refilled only after the next barrier, which every wave reaches after its epilogue)
         // and inserted one by one.
         // every wave (all lanes: qvalid is per lane) passes this barrier exactly once per tile
+        PROF_T(tf);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();                               // all fragment reads of the spent stage done
+        PROF_T(tg);
 #ifdef IMGREC_ABLATE_NO_EPILOGUE
         if (qvalid && row0 < 0) {   // never taken: keeps the accumulators live, no top-k work
 #else
@@ -394,12 +420,12 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
             const float* nrm = norm_base + ((t - t0) % NS) * BM;
             float* park = const_cast<float*>(st) + wave * (PR * 64);
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
+            for (int b = 0; b < WB; ++b) {
                 float key[16];
                 unsigned mask = 0;
                 const float tau = kd[KM - 1];
                 const float tau_p = __shfl_xor(tau, 32, 64);
-                const int rb = wr * 128 + b * 32 + 4 * lh;     // row of accumulator reg 0
+                const int rb = wr * RW + b * 32 + 4 * lh;      // row of accumulator reg 0
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {                  // regs 4j..4j+3 = rows rb+8j+0..3
                     float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -443,8 +469,18 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                 }
             }
         }
+#ifdef IMGREC_PROF
+        PROF_T(th);
+        PROF_ADD(4, tg - tf); PROF_ADD(5, th - tg);
+#endif
     }
 
+#ifdef IMGREC_PROF
+    PROF_T(tk1);
+    prof[6] = tk1 - tk0;
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_prof[i], prof[i]);
+#endif
     if (qvalid) {
         const size_t base = (size_t)qcol * ncand + (size_t)((split * WR + wr) * 2 + lh) * KM;
 #pragma unroll
@@ -585,11 +621,11 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
     return hipGetLastError();
 }
 
-template <int WR, int WQ, int NS, int BK, bool SPLIT = false>
+template <int WR, int WQ, int NS, int BK, bool SPLIT = false, int WB = 4>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
-    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, SPLIT>), grid, block, 0, st, a.xb, \
+    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, SPLIT, WB>), grid, block, 0, st, a.xb, \
                        a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
                        a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
     switch (km) {
@@ -612,13 +648,12 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
 
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
     if (a.split) {
-        // split-bf16 candidate pass (knn_refine.hip certifies and reranks its output)
+        // split-bf16 candidate pass (knn_refine.hip certifies and reranks its output); the
+        // staging depth must be the one the split copy was laid out for (a.sbk)
         if (a.dp % 32 != 0 || (a.km != 16 && a.km != 32)) return hipErrorInvalidValue;
-        if (a.wr == 1 && a.wq == 4) return launch_tile_km<1, 4, 2, 32, true>(a.km, a, st);
-#ifdef IMGREC_SPLIT_VARIANTS
-        if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, 3, 32, true>(a.km, a, st);
-        if (a.wr == 2 && a.wq == 4) return launch_tile_km<2, 4, 3, 32, true>(a.km, a, st);
-#endif
+        if (a.sbk != kSplitBK || a.wb != kSplitWB) return hipErrorInvalidValue;
+        if (a.wr == 1 && a.wq == 4)
+            return launch_tile_km<1, 4, kSplitNS, kSplitBK, true, kSplitWB>(a.km, a, st);
         return hipErrorInvalidValue;
     }
     if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)
@@ -665,3 +700,14 @@ hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStr
 }
 
 }  // namespace imgrec
+
+#ifdef IMGREC_PROF
+// Debug build only (tools/prof_phases.py): read and clear the fused kernel's phase counters.
+extern "C" int knn_debug_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(imgrec::g_prof), 8 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -2;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(imgrec::g_prof), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif

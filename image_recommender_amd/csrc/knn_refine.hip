@@ -5,8 +5,9 @@
 // fewer matrix cycles than the exact v_mfma_f32_32x32x2_f32 form, and keeps the K' best
 // approximate keys per query (K' > k).  This file turns that candidate set into the exact answer:
 //
-//   split_rows      fp32 rows -> split layout (per 32-deep stage, per lane half h and MFMA k-step
-//                   s: a 16-B hi chunk and a 16-B lo chunk holding depth 32j + 16s + 8h + 0..7).
+//   split_rows      fp32 rows -> split layout (per BK-deep stage j, lane half h and MFMA k-step
+//                   s < BK/16: a 16-B hi chunk and a 16-B lo chunk, logical chunks
+//                   h*(BK/8) + 2s and +1, holding depth BK*j + 16s + 8h + 0..7).
 //   rerank_certify  one wave per query: exact fp32 keys of the K' candidates (the same
 //                   faiss exhaustive_L2sqr_blas key form as the exact kernel), top-k by
 //                   (key, label), and a certificate that no row outside the candidate set can
@@ -34,16 +35,18 @@ __device__ __forceinline__ uint32_t bf16_rne(float x) {
     return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
-// one thread per (row, 32-deep stage j, lane half h, k-step s): 8 floats in, 32 B out
+// one thread per (row, BK-deep stage j, lane half h, k-step s): 8 floats in, 32 B out
 __global__ void __launch_bounds__(256)
-split_rows_kernel(const float* __restrict__ src, int64_t n, int dp, uint32_t* __restrict__ dst) {
-    const int per_row = dp / 8;                      // (dp/32) stages x 4 (h, s) pairs
+split_rows_kernel(const float* __restrict__ src, int64_t n, int dp, int bk,
+                  uint32_t* __restrict__ dst) {
+    const int per_row = dp / 8;                      // (dp/bk) stages x 2 halves x bk/16 k-steps
+    const int ks = bk / 16;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n * per_row) return;
     const int64_t row = t / per_row;
     const int r = (int)(t - row * per_row);
-    const int j = r >> 2, h = (r >> 1) & 1, s = r & 1;
-    const float* x = src + row * dp + j * 32 + 16 * s + 8 * h;
+    const int j = r / (2 * ks), h = (r / ks) & 1, s = r % ks;
+    const float* x = src + row * dp + j * bk + 16 * s + 8 * h;
     const float4 v0 = *reinterpret_cast<const float4*>(x);
     const float4 v1 = *reinterpret_cast<const float4*>(x + 4);
     const float e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -56,8 +59,8 @@ split_rows_kernel(const float* __restrict__ src, int64_t n, int dp, uint32_t* __
         hi[p] = h0 | (h1 << 16);
         lo[p] = l0 | (l1 << 16);
     }
-    // logical chunk h*4 + 2s (hi) and +1 (lo): 32 contiguous bytes
-    uint32_t* o = dst + row * dp + j * 32 + (h * 4 + 2 * s) * 4;
+    // logical chunk h*2ks + 2s (hi) and +1 (lo): 32 contiguous bytes
+    uint32_t* o = dst + row * dp + j * bk + (h * 2 * ks + 2 * s) * 4;
     *reinterpret_cast<uint4*>(o) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
     *reinterpret_cast<uint4*>(o + 4) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
 }
@@ -218,12 +221,13 @@ __global__ void max_norm_kernel(const float* __restrict__ xn, int64_t n, float* 
 }
 
 // ---------------------------------------------------------------------------------------------
-hipError_t launch_split_rows(const float* src, int64_t n, int dp, uint32_t* dst, hipStream_t st) {
+hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32_t* dst,
+                             hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    if (dp % 32 != 0) return hipErrorInvalidValue;
+    if ((bk != 16 && bk != 32) || dp % bk != 0) return hipErrorInvalidValue;
     const int64_t threads = n * (dp / 8);
     hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st,
-                       src, n, dp, dst);
+                       src, n, dp, bk, dst);
     return hipGetLastError();
 }
 
