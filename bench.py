@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--single-query-steps", type=int, default=50)
-    ap.add_argument("--mode", choices=("auto", "exact", "split"), default="auto",
+    ap.add_argument("--mode", choices=("auto", "exact", "split", "bf16"), default="auto",
                     help="search arithmetic (include/imgrec_knn.h knn_search_mode)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed steps (for rocprofv3 runs)")
@@ -180,18 +180,22 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
     }
 
 
-def pmc_traffic(kernel_prefix: str, split: bool):
+def pmc_traffic(wr: int, wq: int, path: int):
     """HBM bytes per launch of the fused kernel from the newest profiles/*_traffic.json written by
-    tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None."""
+    tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None.
+    Kernel names are knn_tile_topk_kernel<WR, WQ, KM, NS, BK, MODE, WB> (MODE 0 fp32, 1 split,
+    2 bf16)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=os.path.getmtime)
+    import re
+    pat = re.compile(rf"knn_tile_topk_kernel<{wr}, {wq}, \d+, \d+, \d+, {path}, \d+>")
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
     for f in reversed(files):
         try:
             data = json.load(open(f))
         except Exception:
             continue
         for name, rec in data.items():
-            if name.startswith(kernel_prefix) and name.endswith("true>" if split else "false>"):
+            if pat.search(name):
                 return rec["hbm_bytes_per_launch"], os.path.basename(f)
     return None
 
@@ -250,6 +254,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     split_q, fallback_q, err_ratio = shard.index.search_stats(with_error=True)   # last step
+    path = lib.knn_last_path(shard.index.handle)          # 0 exact, 1 split, 2 bf16
     import ctypes as C
     tot_ms, nl = C.c_double(), C.c_int()
     _lib.check(lib.knn_kernel_time(shard.index.handle, C.byref(tot_ms), C.byref(nl)), "timing")
@@ -307,12 +312,17 @@ def main():
         n_local = shard.local_rows
         flops = 2.0 * n_local * D_total * a.nq
         split = split_q > 0
-        kname = f"void imgrec::knn_tile_topk_kernel<{tr.value // 128}, {tq.value // 32}"
-        traffic = pmc_traffic(kname, split) if world == 1 else None
+        traffic = pmc_traffic(tr.value // 128, tq.value // 32, path) if world == 1 else None
         achieved = flops / (kern_ms * 1e-3) / 1e12
-        # the split kernel issues 3 bf16 MFMAs per fp32-equivalent product (hi.hi + hi.lo + lo.hi):
-        # its matrix-pipe ceiling for the algorithmic 2NDQ flop is the bf16 dense peak / 3
-        peak = MFMA_BF16_PEAK_TFLOPS / 3 if split else MFMA_F32_PEAK_TFLOPS
+        # matrix-pipe ceiling for the algorithmic 2NDQ flop: bf16 path one bf16 MFMA per product
+        # (bf16 dense peak); split path three (hi.hi + hi.lo + lo.hi: bf16 peak / 3); exact path
+        # the fp32 MFMA peak
+        peak = {2: MFMA_BF16_PEAK_TFLOPS, 1: MFMA_BF16_PEAK_TFLOPS / 3}.get(path, MFMA_F32_PEAK_TFLOPS)
+        peak_basis = {2: "bf16 dense MFMA 2516.8 TF/s (one MFMA per product)",
+                      1: "bf16 dense MFMA 2516.8 TF/s / 3 MFMAs per product"}.get(
+                          path, "fp32 dense MFMA (v_mfma_f32_32x32x2_f32)")
+        dtype = {2: "bf16 candidates (fp32 accumulate) + fp32 rerank, certified exact",
+                 1: "bf16x3 split (fp32-equivalent) + fp32 rerank"}.get(path, "fp32")
         bytes1 = 4.0 * n_local * D_total + 4.0 * n_local
         qps = a.nq * a.steps / elapsed
         out = {
@@ -326,10 +336,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16x3 split (fp32-equivalent) + fp32 rerank" if split else "fp32",
+            "dtype": dtype,
             "search_mode": a.mode,
-            "split_path": {"queries": split_q, "certificate_fallbacks": fallback_q,
-                           "max_err_over_bound": err_ratio} if split else None,
+            "search_path": {0: "exact", 1: "split", 2: "bf16"}.get(path, "?"),
+            "candidate_path": {"queries": split_q, "certificate_fallbacks": fallback_q,
+                               "max_err_over_bound": err_ratio} if split else None,
             "data": "synthetic, generated on device (Gaussian-mixture parts, per-part L2-normalised)",
             "config": {
                 "workload": cfg["name"], "rows": cfg["rows"], "dim": D_total, "k": a.k,
@@ -344,12 +355,10 @@ def main():
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": peak,
                 "unit": "TFLOP/s", "frac": achieved / peak,
-                "peak_basis": ("bf16 dense MFMA 2516.8 TF/s / 3 MFMAs per product" if split
-                               else "fp32 dense MFMA (v_mfma_f32_32x32x2_f32)"),
+                "peak_basis": peak_basis,
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
-                "kernel": f"knn_tile_topk_kernel<{tr.value // 128},{tq.value // 32},...,"
-                          f"{'true' if split else 'false'}>",
+                "kernel": f"knn_tile_topk_kernel<{tr.value // 128},{tq.value // 32},...,mode {path}>",
                 "kernel_ms": kern_ms,
                 "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
             },

@@ -17,7 +17,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / os.environ.get("IMGREC_LIB_
 KNN_OK, KNN_EINVAL, KNN_EHIP, KNN_ENOMEM, KNN_EIO, KNN_ENOSYS = 0, -1, -2, -3, -4, -5
 KNN_METRIC_IP, KNN_METRIC_L2, KNN_METRIC_COSINE = 0, 1, 2
 KNN_MAX_K = 32
-KNN_SEARCH_AUTO, KNN_SEARCH_EXACT, KNN_SEARCH_SPLIT = 0, 1, 2
+KNN_SEARCH_AUTO, KNN_SEARCH_EXACT, KNN_SEARCH_SPLIT, KNN_SEARCH_BF16 = 0, 1, 2, 3
 COLOR_HIST_MAX_BINS = 32
 INGEST_NOT_FAST, INGEST_TOO_SMALL = -1, -2
 
@@ -51,6 +51,7 @@ SIGNATURES = {
     "knn_plan": (_i, [_vp, _i64, _i, _pi, _pi, _pi, _pi]),
     "knn_set_search_mode": (_i, [_vp, _i]),
     "knn_search_stats": (_i, [_vp, _pi64, _pi64, _pf]),
+    "knn_last_path": (_i, [_vp]),
     "knn_last_error": (C.c_char_p, []),
     "knn_version": (C.c_char_p, []),
     # imgrec_color.h

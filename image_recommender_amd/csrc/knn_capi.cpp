@@ -147,6 +147,37 @@ inline float rerank_coef(int dp) {
     return (float)(1.02 * (4.0 * ((dp + 255) / 256) + 8.0) * std::ldexp(1.0, -24));
 }
 
+// bf16 candidate pass (one bf16 MFMA per product): the products of two bf16 values are exact in
+// fp32, so the only arithmetic error besides the operand rounding (bounded in the rerank kernel
+// from the stored residual norms) is the fp32 accumulation: 1.02 * gamma_n, n = (dpb/16) MFMAs x 5
+// (a 16-term tree inside each) + 16, with unit roundoff 2^-23 (allows truncating accumulation),
+// relative to |qh| |xh|.
+inline float b16_acc_coef(int dpb) {
+    return (float)(1.02 * (5.0 * (dpb / 16) + 16.0) * std::ldexp(1.0, -23));
+}
+// Candidates the bf16 pass hands to the rerank (K'), and the per-lane list length of its fused
+// kernel (the merge floor covers what a lane list drops).
+constexpr int kB16Cand = 64;
+inline int b16_km(int k) { return k <= 16 ? 16 : 32; }
+
+// bf16-path geometry: (kB16WR, kB16WQ) workgroups, kB16WGPCU per CU.
+Plan make_b16_plan(int64_t ntotal, int64_t nq, int km, int cus) {
+    Plan p{};
+    p.km = km;
+    p.wr = imgrec::kB16WR;
+    p.wq = imgrec::kB16WQ;
+    p.bm = p.wr * 32 * imgrec::kB16WB;
+    p.bq = p.wq * 32;
+    p.nqb = (int)((nq + p.bq - 1) / p.bq);
+    p.nq_pad = p.nqb * p.bq;
+    p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+    const int target = cus * imgrec::kB16WGPCU;
+    p.nsplit = std::max(1, std::min((target + p.nqb - 1) / p.nqb, p.ntiles));
+    p.ncand = p.nsplit * p.wr * 2 * p.km;
+    p.wgs = p.nqb * p.nsplit;
+    return p;
+}
+
 }  // namespace
 
 struct knn_index {
@@ -156,9 +187,14 @@ struct knn_index {
     float* xb = nullptr;     // cap x dp
     float* xn = nullptr;     // cap
     uint32_t* xs = nullptr;  // cap x dp split-bf16 copy (split_ok only)
+    uint16_t* xh = nullptr;  // cap x dpb bf16 copy (b16_ok only)
+    float* xr = nullptr;     // cap: |x - bf16(x)| per row (b16_ok only)
     float* xn_max = nullptr; // device scalar, max |x|^2 (refreshed when rows change)
-    bool split_ok = false, xn_max_stale = true;
+    float* xr_max = nullptr; // device scalar, max |x - bf16(x)|
+    int dpb = 0;             // bf16 row stride (elements)
+    bool split_ok = false, b16_ok = false, xn_max_stale = true;
     int mode = KNN_SEARCH_AUTO;
+    int last_path = 0;       // knn_last_path
     int64_t last_fallback = 0, last_split_queries = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
@@ -174,6 +210,16 @@ struct knn_index {
     int* fail = nullptr; size_t fail_cap = 0;          // [0] = count, [1..] = list
     float* err_ratio = nullptr; size_t err_ratio_cap = 0;
     float last_err_ratio = 0.f;
+    uint16_t* qb16 = nullptr; size_t qb16_cap = 0;
+    float* q_resid = nullptr; size_t q_resid_cap = 0;
+    float* floor = nullptr; size_t floor_cap = 0;
+    size_t xr_max_cap = 0;
+    // cascade workspace (queries a candidate pass could not certify, re-run by the next path)
+    float* cs_q = nullptr; size_t cs_q_cap = 0;
+    float* cs_qn = nullptr; size_t cs_qn_cap = 0;
+    float* cs_d = nullptr; size_t cs_d_cap = 0;
+    int64_t* cs_i = nullptr; size_t cs_i_cap = 0;
+    int* cs_list = nullptr; size_t cs_list_cap = 0;
     float* fb_q = nullptr; size_t fb_q_cap = 0;
     float* fb_qn = nullptr; size_t fb_qn_cap = 0;
     float* fb_d = nullptr; size_t fb_d_cap = 0;
@@ -211,6 +257,19 @@ int reserve_rows(knn_index* ix, int64_t need) {
         }
         KNN_HIP(hipMemsetAsync(nxs, 0, (size_t)ncap * ix->dp * sizeof(uint32_t), ix->stream));
     }
+    uint16_t* nxh = nullptr;
+    float* nxr = nullptr;
+    if (ix->b16_ok) {
+        e = hipMalloc((void**)&nxh, (size_t)ncap * ix->dpb * sizeof(uint16_t));
+        if (e == hipSuccess) e = hipMalloc((void**)&nxr, (size_t)ncap * sizeof(float));
+        if (e != hipSuccess) {
+            for (void* p : {(void*)nxb, (void*)nxn, (void*)nxs, (void*)nxh})
+                if (p) (void)hipFree(p);
+            KNN_FAIL(KNN_ENOMEM, "hipMalloc of the %lld-row bf16 copy failed", (long long)ncap);
+        }
+        KNN_HIP(hipMemsetAsync(nxh, 0, (size_t)ncap * ix->dpb * sizeof(uint16_t), ix->stream));
+        KNN_HIP(hipMemsetAsync(nxr, 0, (size_t)ncap * sizeof(float), ix->stream));
+    }
     KNN_HIP(hipMemsetAsync(nxb, 0, (size_t)ncap * ix->dp * sizeof(float), ix->stream));
     KNN_HIP(hipMemsetAsync(nxn, 0, (size_t)ncap * sizeof(float), ix->stream));
     if (ix->ntotal > 0) {
@@ -221,14 +280,24 @@ int reserve_rows(knn_index* ix, int64_t need) {
         if (nxs)
             KNN_HIP(hipMemcpyAsync(nxs, ix->xs, (size_t)ix->ntotal * ix->dp * sizeof(uint32_t),
                                    hipMemcpyDeviceToDevice, ix->stream));
+        if (nxh) {
+            KNN_HIP(hipMemcpyAsync(nxh, ix->xh, (size_t)ix->ntotal * ix->dpb * sizeof(uint16_t),
+                                   hipMemcpyDeviceToDevice, ix->stream));
+            KNN_HIP(hipMemcpyAsync(nxr, ix->xr, (size_t)ix->ntotal * sizeof(float),
+                                   hipMemcpyDeviceToDevice, ix->stream));
+        }
     }
     KNN_HIP(hipStreamSynchronize(ix->stream));
     if (ix->xb) (void)hipFree(ix->xb);
     if (ix->xn) (void)hipFree(ix->xn);
     if (ix->xs) (void)hipFree(ix->xs);
+    if (ix->xh) (void)hipFree(ix->xh);
+    if (ix->xr) (void)hipFree(ix->xr);
     ix->xb = nxb;
     ix->xn = nxn;
     ix->xs = nxs;
+    ix->xh = nxh;
+    ix->xr = nxr;
     ix->cap = ncap;
     return KNN_OK;
 }
@@ -270,7 +339,7 @@ int exact_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
     a.qp = qpad; a.qnorm = qnorm; a.nq = (int)nq; a.metric = kmetric;
     a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
-    a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.split = false;
+    a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.mode = imgrec::kModeF32;
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
     KNN_HIP(imgrec::launch_tile_topk(a, st));
@@ -280,11 +349,116 @@ int exact_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     return KNN_OK;
 }
 
+// max |x|^2 (and max bf16 residual) over the stored rows, recomputed after rows change
+int refresh_maxima(knn_index* ix, hipStream_t st) {
+    if (!ix->xn_max_stale) return KNN_OK;
+    int rc;
+    if ((rc = grow(&ix->xn_max, &ix->xn_max_cap, 1)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_max_norm(ix->xn, ix->ntotal, ix->xn_max, st));
+    if (ix->b16_ok) {
+        if ((rc = grow(&ix->xr_max, &ix->xr_max_cap, 1)) != KNN_OK) return rc;
+        KNN_HIP(imgrec::launch_max_norm(ix->xr, ix->ntotal, ix->xr_max, st));
+    }
+    ix->xn_max_stale = false;
+    return KNN_OK;
+}
+
+bool use_b16(const knn_index* ix, int64_t nq, int k) {
+    if (!ix->b16_ok || k > KNN_MAX_K) return false;
+    if (ix->mode == KNN_SEARCH_BF16) return true;
+    return ix->mode == KNN_SEARCH_AUTO && nq > 128 && ix->ntotal >= 16384;
+}
+
 bool use_split(const knn_index* ix, int64_t nq, int k) {
     if (!ix->split_ok || ix->mode == KNN_SEARCH_EXACT || split_kc(k) == 0) return false;
     if (ix->mode == KNN_SEARCH_SPLIT) return true;
-    // auto: batches the (1,4) plan covers, corpora with enough rows to amortise the rerank
-    return nq > 128 && ix->ntotal >= 16384;
+    // auto (when the bf16 path is unavailable): batches the (1,4) plan covers, corpora with
+    // enough rows to amortise the rerank
+    return ix->mode == KNN_SEARCH_AUTO && nq > 128 && ix->ntotal >= 16384;
+}
+
+int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+                int64_t* I, hipStream_t st, bool timed);
+
+// Re-run the nfail queries listed in `list` (device, indices into qpad) on the next, more precise
+// path — the split path when enough of them fail and it is available, else the exact kernel —
+// and scatter the results back into D, I.  Own workspace: the nested path may use every other.
+int cascade(knn_index* ix, const float* qpad, const float* qnorm, const int* list, int nfail, int k,
+            float* D, int64_t* I, hipStream_t st) {
+    const bool to_split = ix->split_ok && split_kc(k) != 0 && nfail > 128;
+    const int64_t pad = to_split ? make_split_plan(ix->ntotal, nfail, split_kc(k), ix->cus).nq_pad
+                                 : make_plan(ix->ntotal, nfail, k, ix->cus).nq_pad;
+    int rc;
+    if ((rc = grow(&ix->cs_q, &ix->cs_q_cap, (size_t)pad * ix->dp)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cs_qn, &ix->cs_qn_cap, (size_t)pad)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cs_d, &ix->cs_d_cap, (size_t)nfail * k)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cs_i, &ix->cs_i_cap, (size_t)nfail * k)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cs_list, &ix->cs_list_cap, (size_t)nfail)) != KNN_OK) return rc;
+    KNN_HIP(hipMemcpyAsync(ix->cs_list, list, (size_t)nfail * sizeof(int), hipMemcpyDeviceToDevice, st));
+    KNN_HIP(imgrec::launch_gather_rows(qpad, qnorm, ix->dp, ix->cs_list, nfail, pad, ix->cs_q,
+                                       ix->cs_qn, st));
+    const int64_t keep_q = ix->last_split_queries, keep_fb = ix->last_fallback;
+    rc = to_split ? split_chunk(ix, ix->cs_q, ix->cs_qn, nfail, k, ix->cs_d, ix->cs_i, st, false)
+                  : exact_chunk(ix, ix->cs_q, ix->cs_qn, nfail, k, ix->cs_d, ix->cs_i, st, false);
+    ix->last_split_queries = keep_q;
+    ix->last_fallback = keep_fb;
+    if (rc != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_scatter_results(ix->cs_d, ix->cs_i, ix->cs_list, nfail, k, D, I, st));
+    return KNN_OK;
+}
+
+// bf16 candidates (one bf16 MFMA per product) + exact fp32 rerank of K' = 64 + certificate;
+// uncertified queries cascade to the split path / exact kernel.
+int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+              int64_t* I, hipStream_t st, bool timed) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const int km = b16_km(k), kc = kB16Cand;
+    const Plan p = make_b16_plan(ix->ntotal, nq, km, ix->cus);
+    int rc;
+    if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)p.nq_pad * ix->dpb)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->q_resid, &ix->q_resid_cap, (size_t)p.nq_pad)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 1)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->err_ratio, &ix->err_ratio_cap, 1)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_bf16_rows(qpad, p.nq_pad, ix->dp, ix->dpb, ix->qb16, ix->q_resid, st));
+    TileArgs a{};
+    a.wr = p.wr; a.wq = p.wq; a.km = km; a.wb = imgrec::kB16WB; a.mode = imgrec::kModeBF16;
+    a.xb = reinterpret_cast<const float*>(ix->xh); a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
+    a.dp = ix->dpb / 2; a.qp = reinterpret_cast<const float*>(ix->qb16); a.qnorm = qnorm;
+    a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
+    a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(imgrec::launch_tile_topk(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, p.ncand / km, km, p.ncand,
+                                            km, kc, ix->cand2_d, ix->cand2_i, ix->floor, st));
+    KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
+    KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
+    imgrec::RerankArgs r{};
+    r.mode = imgrec::kModeBF16;
+    r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
+    r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
+    r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = b16_acc_coef(ix->dpb);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I; r.fail_count = ix->fail;
+    r.fail_list = ix->fail + 1; r.err_ratio = ix->err_ratio;
+    r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
+    KNN_HIP(imgrec::launch_rerank_certify(r, st));
+    int nfail = 0;
+    float ratio = 0.f;
+    KNN_HIP(hipMemcpyAsync(&nfail, ix->fail, sizeof(int), hipMemcpyDeviceToHost, st));
+    KNN_HIP(hipMemcpyAsync(&ratio, ix->err_ratio, sizeof(float), hipMemcpyDeviceToHost, st));
+    KNN_HIP(hipStreamSynchronize(st));
+    ix->last_err_ratio = std::max(ix->last_err_ratio, ratio);
+    ix->last_split_queries += nq;
+    if (nfail <= 0) return KNN_OK;
+    ix->last_fallback += nfail;
+    return cascade(ix, qpad, qnorm, ix->fail + 1, nfail, k, D, I, st);
 }
 
 // Split-bf16 candidates + exact rerank + certificate; uncertified queries re-run exactly.
@@ -294,11 +468,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     const int kc = split_kc(k);
     const Plan p = make_split_plan(ix->ntotal, nq, kc, ix->cus);
     int rc;
-    if (ix->xn_max_stale) {
-        if ((rc = grow(&ix->xn_max, &ix->xn_max_cap, 1)) != KNN_OK) return rc;
-        KNN_HIP(imgrec::launch_max_norm(ix->xn, ix->ntotal, ix->xn_max, st));
-        ix->xn_max_stale = false;
-    }
+    if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
     if ((rc = grow(&ix->qsplit, &ix->qsplit_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
@@ -313,7 +483,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     a.dp = ix->dp; a.qp = reinterpret_cast<const float*>(ix->qsplit); a.qnorm = qnorm;
     a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
     a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i;
-    a.ncand = p.nsplit * p.wr * 2 * kc; a.split = true;
+    a.ncand = p.nsplit * p.wr * 2 * kc; a.mode = imgrec::kModeSplit;
     a.wb = imgrec::kSplitWB; a.sbk = imgrec::kSplitBK;
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
@@ -325,6 +495,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
     KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
     imgrec::RerankArgs r{};
+    r.mode = imgrec::kModeSplit;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = split_coef(ix->dp);
@@ -367,18 +538,22 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     }
     for (int64_t c0 = 0; c0 < nq; c0 += kQueryChunk) {
         const int64_t cn = std::min(kQueryChunk, nq - c0);
-        const bool split = use_split(ix, cn, k);
+        const bool b16 = use_b16(ix, cn, k);
+        const bool split = !b16 && use_split(ix, cn, k);
         // padding: the query tile of the plan this chunk will run
-        const Plan p = split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
+        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, b16_km(k), ix->cus)
+                     : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                              : make_plan(ix->ntotal, cn, k, ix->cus);
         const int64_t nq_pad = p.nq_pad;
         int rc;
+        if (c0 == 0) ix->last_path = b16 ? 2 : (split ? 1 : 0);
         if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;
         KNN_HIP(imgrec::launch_rows_ingest(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
                                            ix->qpad, ix->qnorm, st));
-        rc = split ? split_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true)
-                   : exact_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true);
+        rc = b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true)
+             : split ? split_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true)
+                     : exact_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true);
         if (rc != KNN_OK) return rc;
     }
     return KNN_OK;
@@ -395,6 +570,9 @@ int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st) 
     if (ix->split_ok)
         KNN_HIP(imgrec::launch_split_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp,
                                           imgrec::kSplitBK, ix->xs + (size_t)ix->ntotal * ix->dp, st));
+    if (ix->b16_ok)
+        KNN_HIP(imgrec::launch_bf16_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp, ix->dpb,
+                                         ix->xh + (size_t)ix->ntotal * ix->dpb, ix->xr + ix->ntotal, st));
     ix->ntotal += n;
     ix->xn_max_stale = true;
     return KNN_OK;
@@ -426,6 +604,8 @@ int knn_create(int d, int metric, int device, knn_index_t** out) {
     ix->metric = metric;
     ix->device = device;
     ix->split_ok = ix->dp % 32 == 0 && d >= 256;
+    ix->b16_ok = d >= 64;
+    ix->dpb = (int)round_up(d, imgrec::kB16Pad);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
@@ -442,6 +622,10 @@ int knn_free(knn_index_t* ix) {
     if (!ix) return KNN_OK;
     DeviceGuard g(ix->device);
     (void)hipStreamSynchronize(ix->stream);
+    for (void* p : {(void*)ix->xh, (void*)ix->xr, (void*)ix->xr_max, (void*)ix->qb16,
+                    (void*)ix->q_resid, (void*)ix->floor, (void*)ix->cs_q, (void*)ix->cs_qn,
+                    (void*)ix->cs_d, (void*)ix->cs_i, (void*)ix->cs_list})
+        if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
                     (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,
                     (void*)ix->qsplit, (void*)ix->cand2_d, (void*)ix->cand2_i, (void*)ix->fail, (void*)ix->err_ratio,
@@ -621,11 +805,14 @@ int knn_kernel_time(knn_index_t* ix, double* total_ms, int* launches) {
 
 int knn_set_search_mode(knn_index_t* ix, int mode) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (mode != KNN_SEARCH_AUTO && mode != KNN_SEARCH_EXACT && mode != KNN_SEARCH_SPLIT)
+    if (mode != KNN_SEARCH_AUTO && mode != KNN_SEARCH_EXACT && mode != KNN_SEARCH_SPLIT &&
+        mode != KNN_SEARCH_BF16)
         KNN_FAIL(KNN_EINVAL, "unknown search mode %d", mode);
     std::lock_guard<std::mutex> lk(ix->mu);
     if (mode == KNN_SEARCH_SPLIT && !ix->split_ok)
         KNN_FAIL(KNN_EINVAL, "split search needs d >= 256 (rows padded to 32 floats); d = %d", ix->d);
+    if (mode == KNN_SEARCH_BF16 && !ix->b16_ok)
+        KNN_FAIL(KNN_EINVAL, "bf16 search needs d >= 64; d = %d", ix->d);
     ix->mode = mode;
     return KNN_OK;
 }
@@ -640,9 +827,14 @@ int knn_search_stats(knn_index_t* ix, int64_t* split_queries, int64_t* fallback_
     return KNN_OK;
 }
 
+int knn_last_path(const knn_index_t* ix) { return ix ? ix->last_path : KNN_EINVAL; }
+
 int knn_plan(const knn_index_t* ix, int64_t nq, int k, int* tr, int* tq, int* splits, int* wgs) {
     if (!ix || !tr || !tq || !splits || !wgs) KNN_FAIL(KNN_EINVAL, "NULL argument");
-    const Plan p = make_plan(ix->ntotal, std::min(nq, kQueryChunk), k, ix->cus);
+    const int64_t cn = std::min(nq, kQueryChunk);
+    const Plan p = use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, b16_km(k), ix->cus)
+                 : use_split(ix, cn, k) ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
+                                        : make_plan(ix->ntotal, cn, k, ix->cus);
     *tr = p.bm;
     *tq = p.bq;
     *splits = p.nsplit;

@@ -7,14 +7,20 @@
 
 namespace imgrec {
 
+// Arithmetic of the fused distance + top-k kernel.
+constexpr int kModeF32 = 0;     // exact fp32 rows, v_mfma_f32_32x32x2_f32
+constexpr int kModeSplit = 1;   // split-bf16 rows (hi, lo), three bf16 MFMAs per product
+constexpr int kModeBF16 = 2;    // bf16 rows, one bf16 MFMA per product (candidate pass)
+
 // Arguments of one fused distance + top-k launch.
 struct TileArgs {
     int wr, wq, km;             // waves along rows / queries, register list length
     int wb = 4;                 // 32-row MFMA blocks per wave (rows per wave = 32*wb)
     int sbk = 0;                // split path: staging depth the split copy is laid out for
-    const float* xb;            // corpus, nrows_cap x dp (rows padded to 256, columns to 16)
+    int mode = kModeF32;        // kMode*: layout of xb / qp and the MFMA form
+    const float* xb;            // corpus, nrows_cap x dp 32-bit words (rows padded to 256)
     const float* xnorm;         // |x|^2 per stored row
-    int nrows, dp;
+    int nrows, dp;              // dp = row stride in 32-bit words (bf16 rows: elements / 2)
     const float* qp;            // queries, nq_pad x dp
     const float* qnorm;         // |q|^2 per padded query
     int nq;
@@ -24,11 +30,11 @@ struct TileArgs {
     float* cand_d;              // nq x ncand keys
     int64_t* cand_i;            // nq x ncand labels
     int ncand;
-    bool split;                 // xb / qp hold the split-bf16 layout (knn_refine.hip)
 };
 
-// One rerank + certificate launch over merged split-path candidates (knn_refine.hip).
+// One rerank + certificate launch over merged candidate-pass candidates (knn_refine.hip).
 struct RerankArgs {
+    int mode;                   // kModeSplit or kModeBF16: which error bound certifies
     const float* qp;            // fp32 padded queries, nq x dp
     const float* qnorm;
     int dp;
@@ -41,7 +47,12 @@ struct RerankArgs {
     int kc;
     int64_t nq;
     int k, metric;              // metric 1 = L2, otherwise inner product
-    float c_split, c_fp;        // relative error-bound coefficients (see knn_capi.cpp)
+    float c_split, c_fp;        // relative error-bound coefficients (see knn_capi.cpp); for
+                                // kModeBF16 c_split is the MFMA accumulation coefficient
+    const float* q_resid;       // kModeBF16: |q - bf16(q)| per query
+    const float* xr_max;        // kModeBF16: device scalar, max over rows of |x - bf16(x)|
+    const float* floor;         // per query: smallest key any row outside the candidates can
+                                // have besides the K'-th candidate's (merge "floor"), or NULL
     float* D;
     int64_t* I;
     int* fail_count;            // device counter (zeroed by the caller)
@@ -64,12 +75,39 @@ constexpr int kDepthPad = 16;       // row stride is rounded to this many floats
 #endif
 constexpr int kSplitBK = IMGREC_SPLIT_BK, kSplitNS = IMGREC_SPLIT_NS, kSplitWB = IMGREC_SPLIT_WB;
 
+// bf16 candidate-pass tile: (kB16WR, kB16WQ) workgroups of kB16WB-block waves, 64-deep stages
+// (32 words), kB16NS ring, kB16WGPCU workgroups per CU; rows of the bf16 copy padded to
+// kB16Pad elements.
+#ifndef IMGREC_B16_WR
+#define IMGREC_B16_WR 1
+#endif
+#ifndef IMGREC_B16_WQ
+#define IMGREC_B16_WQ 4
+#endif
+#ifndef IMGREC_B16_WB
+#define IMGREC_B16_WB 4
+#endif
+#ifndef IMGREC_B16_NS
+#define IMGREC_B16_NS 2
+#endif
+#ifndef IMGREC_B16_WGPCU
+#define IMGREC_B16_WGPCU 2
+#endif
+constexpr int kB16WR = IMGREC_B16_WR, kB16WQ = IMGREC_B16_WQ, kB16WB = IMGREC_B16_WB;
+constexpr int kB16NS = IMGREC_B16_NS, kB16WGPCU = IMGREC_B16_WGPCU, kB16Pad = 64;
+
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st);
 hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st);
+// Candidate merge for the rerank: nq x kout approximate candidates (ascending raw keys, empty =
+// label -1) and, per query, the floor: the smallest key a row dropped by any list or by the merge's
+// own lane lists can have (+inf when nothing was dropped).
+hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
+                                   int kin, int64_t stride_q, int64_t stride_l, int kout,
+                                   float* D, int64_t* I, float* floor, hipStream_t st);
 hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStream_t st);
 
 hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32_t* dst,
@@ -79,6 +117,9 @@ hipError_t launch_gather_rows(const float* src, const float* src_norm, int dp, c
                               int64_t n, int64_t n_pad, float* dst, float* dst_norm, hipStream_t st);
 hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int* list, int64_t n,
                                   int k, float* D, int64_t* I, hipStream_t st);
+// fp32 rows (stride dp) -> bf16 rows (stride dpb elements, zero padded), |x - bf16(x)| per row
+hipError_t launch_bf16_rows(const float* src, int64_t n, int dp, int dpb, uint16_t* dst,
+                            float* resid, hipStream_t st);
 hipError_t launch_max_norm(const float* xn, int64_t n, float* out, hipStream_t st);
 
 }  // namespace imgrec

@@ -217,7 +217,7 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
 #else
 #define IMGREC_MIN_WAVES(nw) ((nw) == 4 ? 2 : 1)
 #endif
-template <int WR, int WQ, int KM, int NS, int BK, bool SPLIT, int WB>
+template <int WR, int WQ, int KM, int NS, int BK, int MODE, int WB>
 __global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
                      int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
@@ -371,7 +371,18 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
             issue_next();                            // refills the buffer the previous stage used
 #endif
             PROF_T(td);
-            if constexpr (SPLIT) {
+            if constexpr (MODE == kModeBF16) {
+                // bf16 rows (2 elements per 32-bit word): this lane half's chunk c holds the 8
+                // elements of MFMA k-step c (depth 32h + 8c + 0..7 of the 64-deep stage, the same
+                // permutation on both operands); one bf16 MFMA per product
+#pragma unroll
+                for (int c = 0; c < CPR / 2; ++c) {
+                    const bf16x8 bv = frag_bf16(bq, c);
+#pragma unroll
+                    for (int b = 0; b < WB; ++b)
+                        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_bf16(a[b], c), bv, acc[b], 0, 0, 0);
+                }
+            } else if constexpr (MODE == kModeSplit) {
                 // split layout: this lane half's chunks 2s / 2s+1 are the hi / lo bf16 planes of
                 // MFMA k-step s; dot ~= hi.hi + hi.lo + lo.hi (the lo.lo term is below the bound)
 #pragma unroll
@@ -541,7 +552,8 @@ template <int KM, int WPQ>
 __global__ void __launch_bounds__(256)
 knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
                  int nlists, int kin, int64_t stride_q, int64_t stride_l, int k, int metric,
-                 int negate_in, float* __restrict__ D, int64_t* __restrict__ I) {
+                 int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
+                 float* __restrict__ floor_out) {
     constexpr int QPB = 4 / WPQ;                     // queries per 256-thread block
     __shared__ float sd[4][KM];
     __shared__ int64_t si[4][KM];
@@ -556,10 +568,15 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
 #pragma unroll
     for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
 
+    // floor (candidate merges only): the smallest key among rows that no output can contain
+    // because a full input list ended before them (its last key) or a lane list dropped them
+    float floor_v = INFINITY;
+    bool dropped = false;
     if (active) {
         for (int l = sub * 64 + lane; l < nlists; l += 64 * WPQ) {
             const float* lp = cd + q * stride_q + (int64_t)l * stride_l;
             const int64_t* ip = ci + q * stride_q + (int64_t)l * stride_l;
+            if (floor_out && ip[kin - 1] >= 0) floor_v = fminf(floor_v, lp[kin - 1]);
             bool stop = false;
             for (int p0 = 0; p0 < kin && !stop; p0 += 8) {
                 float d8[8];
@@ -573,8 +590,10 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float d = negate_in ? -d8[j] : d8[j];
-                    const bool ok = !stop && (p0 + j < kin) && i8[j] >= 0 &&
-                                    ranks_before(d, i8[j], kd[KM - 1], ki[KM - 1]);
+                    const bool real = !stop && (p0 + j < kin) && i8[j] >= 0;
+                    const bool ok = real && ranks_before(d, i8[j], kd[KM - 1], ki[KM - 1]);
+                    // a real entry turned away, or one pushed out of a full lane list
+                    dropped = dropped || (real && (!ok || ki[KM - 1] >= 0));
                     stop = stop || !ok;
                     if (ok) list_insert<KM, int64_t>(kd, ki, d, i8[j]);
                 }
@@ -583,6 +602,12 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
     }
 
     if (WPQ == 1) {
+        if (floor_out) {
+            if (dropped) floor_v = fminf(floor_v, kd[KM - 1]);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) floor_v = fminf(floor_v, __shfl_xor(floor_v, off, 64));
+            if (active && lane == 0) floor_out[q] = floor_v;
+        }
         if (active) wave_select<KM>(kd, ki, k, lane, D + q * k, I + q * k, 1, metric);
         return;
     }
@@ -621,11 +646,11 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
     return hipGetLastError();
 }
 
-template <int WR, int WQ, int NS, int BK, bool SPLIT = false, int WB = 4>
+template <int WR, int WQ, int NS, int BK, int MODE = kModeF32, int WB = 4>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
-    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, SPLIT, WB>), grid, block, 0, st, a.xb, \
+    hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, MODE, WB>), grid, block, 0, st, a.xb, \
                        a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
                        a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
     switch (km) {
@@ -647,13 +672,19 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
 #endif
 
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
-    if (a.split) {
+    if (a.mode == kModeBF16) {
+        // bf16 candidate pass: rows of dp bf16 = dp/2 words, 64-deep (32-word) stages
+        if (a.dp % 32 != 0 || (a.km != 16 && a.km != 32)) return hipErrorInvalidValue;
+        if (a.wb != kB16WB || a.wr != kB16WR || a.wq != kB16WQ) return hipErrorInvalidValue;
+        return launch_tile_km<kB16WR, kB16WQ, kB16NS, 32, kModeBF16, kB16WB>(a.km, a, st);
+    }
+    if (a.mode == kModeSplit) {
         // split-bf16 candidate pass (knn_refine.hip certifies and reranks its output); the
         // staging depth must be the one the split copy was laid out for (a.sbk)
         if (a.dp % 32 != 0 || (a.km != 16 && a.km != 32)) return hipErrorInvalidValue;
         if (a.sbk != kSplitBK || a.wb != kSplitWB) return hipErrorInvalidValue;
         if (a.wr == 1 && a.wq == 4)
-            return launch_tile_km<1, 4, kSplitNS, kSplitBK, true, kSplitWB>(a.km, a, st);
+            return launch_tile_km<1, 4, kSplitNS, kSplitBK, kModeSplit, kSplitWB>(a.km, a, st);
         return hipErrorInvalidValue;
     }
     if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)
@@ -678,10 +709,10 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
     do {                                                                                            \
         if (wide)                                                                                   \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, k, metric, negate_in, D, I);               \
+                               kin, stride_q, stride_l, k, metric, negate_in, D, I, nullptr);      \
         else                                                                                        \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 1>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, k, metric, negate_in, D, I);               \
+                               kin, stride_q, stride_l, k, metric, negate_in, D, I, nullptr);      \
     } while (0)
     if (k <= 8) IMGREC_LAUNCH_MERGE(8);
     else if (k <= 10) IMGREC_LAUNCH_MERGE(10);
@@ -689,6 +720,18 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
     else if (k <= 32) IMGREC_LAUNCH_MERGE(32);
     else return hipErrorInvalidValue;
 #undef IMGREC_LAUNCH_MERGE
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
+                                   int kin, int64_t stride_q, int64_t stride_l, int kout,
+                                   float* D, int64_t* I, float* floor, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (kout <= 0 || kout > 64 || !floor) return hipErrorInvalidValue;
+    // one wave per query; the lane lists hold 32 entries (a lane's lists beyond that are covered
+    // by the floor), the output takes kout rounds of the wave argmin
+    hipLaunchKernelGGL((knn_merge_kernel<32, 1>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
+                       cd, ci, nq, nlists, kin, stride_q, stride_l, kout, 1, 0, D, I, floor);
     return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-// knn_refine.hip — split-bf16 candidate path of the exact k-NN search (gfx950).
+// knn_refine.hip — candidate paths of the exact k-NN search (gfx950): split-bf16 and bf16.
 //
 // The fused kernel (knn_kernels.hip, SPLIT=true) scores every corpus row against every query with
 // three bf16 MFMAs per 16-deep step (x = hi + lo, both bf16; q.x ~= qh.xh + qh.xl + ql.xh), 5.3x
@@ -65,6 +65,46 @@ split_rows_kernel(const float* __restrict__ src, int64_t n, int dp, int bk,
     *reinterpret_cast<uint4*>(o + 4) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
 }
 
+// One wave per row: fp32 row (stride dp words) -> bf16 row (stride dpb elements, RNE, zero
+// padded) and the Euclidean norm of the rounding residual x - bf16(x), accumulated in fp32 (the
+// certificate inflates it, knn_capi.cpp bf16 bound).
+__global__ void __launch_bounds__(256)
+bf16_rows_kernel(const float* __restrict__ src, int64_t n, int dp, int dpb,
+                 uint16_t* __restrict__ dst, float* __restrict__ resid) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const float* x = src + row * dp;
+    uint16_t* o = dst + row * dpb;
+    float acc = 0.f;
+    for (int c = lane; c < dpb / 8; c += 64) {         // 8 elements (16 B out) per lane step
+        float e[8];
+        if (8 * c + 8 <= dp) {
+            const float4 v0 = *reinterpret_cast<const float4*>(x + 8 * c);
+            const float4 v1 = *reinterpret_cast<const float4*>(x + 8 * c + 4);
+            e[0] = v0.x; e[1] = v0.y; e[2] = v0.z; e[3] = v0.w;
+            e[4] = v1.x; e[5] = v1.y; e[6] = v1.z; e[7] = v1.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) e[j] = (8 * c + j < dp) ? x[8 * c + j] : 0.f;
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t h0 = bf16_rne(e[2 * p]), h1 = bf16_rne(e[2 * p + 1]);
+            const float r0 = e[2 * p] - __uint_as_float(h0 << 16);
+            const float r1 = e[2 * p + 1] - __uint_as_float(h1 << 16);
+            acc = fmaf(r0, r0, acc);
+            acc = fmaf(r1, r1, acc);
+            w[p] = h0 | (h1 << 16);
+        }
+        *reinterpret_cast<uint4*>(o + 8 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) resid[row] = sqrtf(acc);
+}
+
 template <typename I>
 __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
     return d1 < d2 || (d1 == d2 && i1 < i2);
@@ -79,7 +119,9 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
                       const float* __restrict__ cd, const int64_t* __restrict__ ci, int kc,
                       int64_t nq, int k, int metric, float c_split, float c_fp,
                       float* __restrict__ D, int64_t* __restrict__ I, int* __restrict__ fail_count,
-                      int* __restrict__ fail_list, float* __restrict__ err_ratio) {
+                      int* __restrict__ fail_list, float* __restrict__ err_ratio, int mode,
+                      const float* __restrict__ q_resid, const float* __restrict__ xr_max,
+                      const float* __restrict__ floor) {
     const int lane = threadIdx.x & 63;
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
@@ -153,8 +195,20 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
     const float xm = *xn_max;
     const float nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
     const float u = 1.0f / 8388608.f;               // 2^-23
+    // |approximate q.x - q.x| for every row:
+    //   split: c_split |q| max|x|
+    //   bf16:  |q.(x - xh) + (q - qh).xh| + accumulation <= |q| R + dq (X + R) + c_acc |qh| |xh|
+    //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max |x|,
+    //          |qh| <= |q| + dq, |xh| <= X + R), inflated for the fp32 evaluation of the bound
+    float e_ip;
+    if (mode == kModeBF16) {
+        const float sq = sqrtf(qn), X = sqrtf(xm), R = *xr_max, dq = q_resid[q];
+        e_ip = (sq * R + dq * (X + R) + c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
+    } else {
+        e_ip = c_split * nn;
+    }
     auto bound_a = [&](float v) {                   // |approx key - exact key| bound at key v
-        return metric == 1 ? 2.f * c_split * nn + 2.f * u * (qn + xm + fabsf(v)) : c_split * nn;
+        return metric == 1 ? 2.f * e_ip + 2.f * u * (qn + xm + fabsf(v)) : e_ip;
     };
     auto bound_f = [&](float v) {                   // |fp32 rerank key - exact key| bound
         return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
@@ -168,10 +222,13 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
         atomicMax(reinterpret_cast<unsigned*>(err_ratio), __float_as_uint(r));
     }
 
-    // certificate (a full candidate set only: fewer than kc candidates means every row is one)
+    // certificate: tau = smallest approximate key a row outside the candidates can have — the
+    // K'-th candidate's (when the set is full) and the merge floor (rows dropped by full lists);
+    // +inf means every row is a candidate
     const int64_t lab_tau = ci[q * kc + kc - 1];
-    if (lab_tau < 0 || nvalid < kc) return;
-    const float tau = cd[q * kc + kc - 1];
+    float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
+    if (floor) tau = fminf(tau, floor[q]);
+    if (tau == INFINITY) return;
     float sk = (valid && rank == k - 1) ? key : -INFINITY;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
@@ -237,7 +294,7 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(rerank_certify_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, st,
                        a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci, a.kc,
                        a.nq, a.k, a.metric, a.c_split, a.c_fp, a.D, a.I, a.fail_count, a.fail_list,
-                       a.err_ratio);
+                       a.err_ratio, a.mode, a.q_resid, a.xr_max, a.floor);
     return hipGetLastError();
 }
 
@@ -254,6 +311,15 @@ hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int*
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(scatter_results_kernel, dim3((unsigned)((n * k + 255) / 256)), dim3(256), 0,
                        st, sd, si, list, n, k, D, I);
+    return hipGetLastError();
+}
+
+hipError_t launch_bf16_rows(const float* src, int64_t n, int dp, int dpb, uint16_t* dst,
+                            float* resid, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (dpb % 8 != 0 || dp % 8 != 0 || dpb < dp) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bf16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, n, dp,
+                       dpb, dst, resid);
     return hipGetLastError();
 }
 

@@ -170,7 +170,7 @@ class Index:
 
     # -- search arithmetic (extension; include/imgrec_knn.h knn_search_mode) -------------------
     SEARCH_MODES = {"auto": _lib.KNN_SEARCH_AUTO, "exact": _lib.KNN_SEARCH_EXACT,
-                    "split": _lib.KNN_SEARCH_SPLIT}
+                    "split": _lib.KNN_SEARCH_SPLIT, "bf16": _lib.KNN_SEARCH_BF16}
 
     @property
     def search_mode(self) -> str:
@@ -185,7 +185,8 @@ class Index:
         self._mode = mode
 
     def search_stats(self, with_error: bool = False):
-        """(queries of the last search on the split path, of which re-run on the exact kernel)
+        """(queries of the last search on a candidate path (split / bf16), of which re-run on a
+        more precise path because their certificate failed)
         [+ largest observed approximation error / certificate bound, with_error=True]."""
         a, b, r = C.c_int64(), C.c_int64(), C.c_float()
         _lib.check(_lib.load().knn_search_stats(self._h, C.byref(a), C.byref(b), C.byref(r)),

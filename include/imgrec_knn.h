@@ -58,17 +58,22 @@ enum knn_error {
     KNN_ENOSYS = -5    /* not supported (e.g. no GPU visible) */
 };
 
-/* Search arithmetic.  AUTO: batches of > 128 queries with k <= 16 on an index with d >= 256 take
- * the split path (bf16 hi/lo candidate pass, exact fp32 rerank of K' candidates and a per-query
- * error-bound certificate; uncertified queries re-run on the exact kernel), everything else the
- * exact fp32 kernel.  Both return the same results up to fp32 rounding of the distances: the
- * certificate guarantees the candidate set contains every row the exact search could return.
- * EXACT: always the fp32 kernel.  SPLIT: the split path whenever k <= 16 (tests).
- * A split-path search synchronises its stream once per 8192-query chunk (certificate count). */
+/* Search arithmetic.  Every mode returns the exact search's results (same labels; distances are
+ * fp32 values of the same key): a candidate pass proposes K' rows per query, an fp32 rerank
+ * computes their exact keys and a per-query error-bound certificate proves that no row outside
+ * the candidates can rank before a returned one; uncertified queries re-run on a more precise
+ * path (bf16 -> split when more than 128 fail, else -> exact fp32 kernel).
+ * AUTO: batches of > 128 queries on an index of >= 16384 rows take the bf16 path (d >= 64; one
+ *       bf16 MFMA per product, K' = 64), or the split path when bf16 is unavailable; everything
+ *       else the exact fp32 kernel.
+ * EXACT: always the fp32 kernel.  SPLIT: the split path (bf16 hi/lo, three MFMAs per product,
+ *       K' = 16/32) whenever k <= 16 and d >= 256.  BF16: the bf16 path for every batch (tests).
+ * A candidate-path search synchronises its stream once per 8192-query chunk (certificate count). */
 enum knn_search_mode {
     KNN_SEARCH_AUTO = 0,
     KNN_SEARCH_EXACT = 1,
-    KNN_SEARCH_SPLIT = 2
+    KNN_SEARCH_SPLIT = 2,
+    KNN_SEARCH_BF16 = 3
 };
 
 /* Largest k one search can return (the fused top-k keeps per-lane lists of this length). */
@@ -126,12 +131,16 @@ int knn_set_timing(knn_index_t* index, int enable);
 int knn_kernel_time(knn_index_t* index, double* total_ms, int* launches);
 
 int knn_set_search_mode(knn_index_t* index, int mode);
-/* Queries of the last search that took the split path, how many of them failed the certificate
- * and were re-run on the exact kernel, and (may be NULL) the largest observed
+/* Queries of the last search that took a candidate path (split or bf16), how many of them failed
+ * the certificate and were re-run on a more precise path, and (may be NULL) the largest observed
  * |approximate key - fp32 key| / (error bound of both) over all candidates: <= 1 whenever the
  * certificate's bounds hold, in practice far below. */
 int knn_search_stats(knn_index_t* index, int64_t* split_queries, int64_t* fallback_queries,
                      float* max_err_ratio);
+
+/* Arithmetic the last search's first query chunk ran: 0 = exact fp32 kernel, 1 = split path,
+ * 2 = bf16 path (the candidate paths' fallbacks are counted by knn_search_stats). */
+int knn_last_path(const knn_index_t* index);
 
 /* Launch geometry chosen for a search of nq queries (for reports): workgroup tile rows/queries,
  * row splits and workgroup count. */

@@ -1,0 +1,199 @@
+"""Parity tests of the bf16 candidate path (include/imgrec_knn.h KNN_SEARCH_BF16, the AUTO default
+for large batches).
+
+The bf16 path scores rows with ONE bf16 MFMA per product, reranks K' = 64 candidates in exact fp32
+and certifies per query, from the stored residual norms |x - bf16(x)|, that no row outside the
+candidates can rank before a returned one; uncertified queries cascade to the split path (more than
+128 of them) or the exact kernel.  Results must satisfy the SAME contract as the exact path
+(tests/knn_check.py against the float64 oracle): the arithmetic is an implementation detail of the
+reference's index.search (main/search_from_image.py:247).
+"""
+import numpy as np
+import pytest
+
+from tests.datagen import concat_rows, mixture
+from tests.knn_check import check_knn
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def faiss(gpu):
+    from image_recommender_amd import faiss_compat
+    return faiss_compat
+
+
+def _bound_holds(idx):
+    ncand, _, ratio = idx.search_stats(with_error=True)
+    if ncand:
+        assert 0.0 <= ratio < 1.0, ratio
+
+
+def _index(faiss, d, metric):
+    if metric == "l2":
+        return faiss.IndexFlatL2(d)
+    if metric == "ip":
+        return faiss.IndexFlatIP(d)
+    return faiss.IndexFlat(d, faiss.METRIC_COSINE)
+
+
+@pytest.mark.parametrize("d", [64, 100, 256, 768, 1968])
+@pytest.mark.parametrize("nq", [1, 130, 300])
+def test_bf16_l2_shapes(faiss, d, nq):
+    xb = mixture(6000, d, centres=50, seed=d)
+    xq = mixture(nq, d, centres=50, seed=d + 1)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    assert idx.search_stats()[0] == nq
+    _bound_holds(idx)
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 32])
+def test_bf16_k_values(faiss, k):
+    xb = mixture(8000, 512, centres=80, seed=k)
+    xq = mixture(260, 512, centres=80, seed=k + 100)
+    idx = faiss.IndexFlatL2(512)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, k)
+    assert idx.search_stats()[0] == 260
+    _bound_holds(idx)
+    check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("metric", ["ip", "cosine"])
+def test_bf16_ip_and_cosine(faiss, metric):
+    xb = mixture(7000, 384, centres=40, seed=5)
+    xq = mixture(300, 384, centres=40, seed=6)
+    idx = _index(faiss, 384, metric)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    _bound_holds(idx)
+    check_knn(D, I, xb, xq, 10, metric, min_exact_frac=0.5)
+    assert np.all(np.diff(D, axis=1) <= 0)
+
+
+def test_bf16_concat_layout_self_query(faiss):
+    """Config-3 rows (48|128|1792 unit parts): self match at rank 0 with 4 - 2*sqrt(3), and the
+    certificate holds for (almost) every query on this layout."""
+    xb = concat_rows(20000, seed=11)
+    q = xb[:300].copy()
+    faiss.normalize_L2(q)
+    idx = faiss.IndexFlatL2(xb.shape[1])
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(q, 10)
+    ncand, nfb = idx.search_stats()
+    assert ncand == 300 and nfb <= 30
+    _bound_holds(idx)
+    check_knn(D, I, xb, q, 10, "l2", min_exact_frac=0.5)
+    assert (I[:, 0] == np.arange(300)).all()
+    np.testing.assert_allclose(D[:, 0], 4 - 2 * np.sqrt(3), rtol=0, atol=1e-5)
+
+
+def test_bf16_cascade_through_split_on_ties(faiss):
+    """Every row duplicated 80 times (more than K' = 64): no certificate can hold; 150 > 128
+    failures cascade to the split path, which fails too and re-runs exactly; ties still break by
+    the smaller label."""
+    base = mixture(200, 256, centres=20, seed=9)
+    xb = np.repeat(base, 80, axis=0)
+    xq = base[:150] + np.float32(1e-3)
+    idx = faiss.IndexFlatL2(256)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    ncand, nfb = idx.search_stats()
+    assert ncand == 150 and nfb == 150
+    check_knn(D, I, xb, xq, 10, "l2")
+    assert (I == np.arange(150)[:, None] * 80 + np.arange(10)[None, :]).all()
+
+
+def test_bf16_partial_fallback_matches_exact(faiss):
+    """A few uncertified queries among certified ones: the exact re-runs scatter into place."""
+    rng = np.random.default_rng(4)
+    xb = mixture(12000, 512, centres=100, seed=4)
+    xb[6000:6300] = xb[6000]                              # one block of 300 duplicates (> K')
+    xq = np.concatenate([mixture(250, 512, centres=100, seed=5), xb[6000:6040] + 1e-4])
+    xq = xq[rng.permutation(len(xq))].astype(np.float32)
+    idx = faiss.IndexFlatL2(512)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    ncand, nfb = idx.search_stats()
+    assert ncand == 290 and 40 <= nfb < 290
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+    idx.search_mode = "exact"
+    De, Ie = idx.search(xq, 10)
+    assert (I == Ie).mean() > 0.95
+
+
+def test_bf16_neighbours_packed_in_one_list(faiss):
+    """40 near neighbours of each query placed on rows that all feed ONE per-lane list of the fused
+    kernel (rows 8m + 0): the list keeps 16, the merge floor must stop a false certificate."""
+    d = 256
+    rng = np.random.default_rng(7)
+    xb = mixture(30000, d, centres=30, seed=7)
+    xq = mixture(140, d, centres=30, seed=8)
+    for qi in range(0, 140, 7):
+        rows = 8 * np.arange(40) + 320 * (qi // 7) + 1000
+        xb[rows] = xq[qi] + (0.002 * (1 + np.arange(40))[:, None] *
+                             rng.standard_normal((40, d))).astype(np.float32)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    for k in (10, 16, 32):
+        D, I = idx.search(xq, k)
+        _bound_holds(idx)
+        check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)
+
+
+def test_bf16_after_incremental_adds_and_regrowth(faiss):
+    xb = mixture(9000, 768, centres=60, seed=21)
+    idx = faiss.IndexFlatL2(768)
+    for part in np.array_split(xb, 5):                    # forces buffer regrowth copies
+        idx.add(part)
+    idx.search_mode = "bf16"
+    xq = mixture(140, 768, centres=60, seed=22)
+    D, I = idx.search(xq, 10)
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+    idx.reset()
+    idx.add(xb[:500])
+    D, I = idx.search(xq, 5)
+    check_knn(D, I, xb[:500], xq, 5, "l2", min_exact_frac=0.5)
+
+
+def test_bf16_tiny_corpus_and_id_offset(faiss):
+    xb = mixture(12, 256, seed=3)
+    idx = faiss.IndexFlatL2(256)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xb[:5], 10)
+    check_knn(D, I, xb, xb[:5], 10, "l2")
+    idx.set_id_offset(1000)
+    D2, I2 = idx.search(xb[:5], 10)
+    np.testing.assert_array_equal(I2, I + 1000)
+    np.testing.assert_array_equal(D2, D)
+
+
+def test_bf16_large_values_scale_invariant(faiss):
+    """Rows with norms ~1e3 (not unit): the bound scales with |q| max|x|, results stay exact."""
+    xb = mixture(10000, 300, centres=40, seed=12) * np.float32(800.0)
+    xq = mixture(200, 300, centres=40, seed=13) * np.float32(800.0)
+    idx = faiss.IndexFlatL2(300)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    _bound_holds(idx)
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+
+
+def test_bf16_mode_rejected_for_tiny_d(faiss):
+    idx = faiss.IndexFlatL2(32)
+    with pytest.raises(faiss.KnnError):
+        idx.search_mode = "bf16"
+    with pytest.raises(ValueError):
+        idx.search_mode = "fp8"

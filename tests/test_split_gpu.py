@@ -166,6 +166,8 @@ def test_split_tiny_corpus_and_id_offset(faiss):
 
 
 def test_auto_mode_routing(faiss):
+    """AUTO: large batches take a candidate path (bf16 when available), small ones the exact
+    kernel."""
     xb = mixture(20000, 512, centres=100, seed=31)
     idx = faiss.IndexFlatL2(512)
     idx.add(xb)
@@ -183,4 +185,4 @@ def test_split_mode_rejected_for_small_d(faiss):
     with pytest.raises(faiss.KnnError):
         idx.search_mode = "split"
     with pytest.raises(ValueError):
-        idx.search_mode = "bf16"
+        idx.search_mode = "tf32"

@@ -1,0 +1,15 @@
+#!/bin/bash
+# bf16-path round: its parity tests first, then the full GPU suite, bench, kernel-stats profile.
+set -u
+export PYTHONPATH=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
+TAG=${1:-b16}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_bf16_gpu.py -x -v --timeout 120 --timeout-method thread > $OUT/pytest_b16.log 2>&1 || { echo "bf16 pytest failed"; tail -40 $OUT/pytest_b16.log; exit 1; }
+tail -2 $OUT/pytest_b16.log
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 2; }
+cat $OUT/bench.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo "rocprof failed"; exit 3; }
+head -8 $OUT/prof/run_kernel_stats.csv | cut -c1-220
