@@ -1,0 +1,336 @@
+// knn_b16.hip — 256 x 256-tile bf16 candidate kernel of the k-NN search (gfx950 / MI355X).
+//
+// Same contract as knn_tile_topk_kernel<..., kModeBF16, ...> (knn_kernels.hip): score every corpus
+// row of the workgroup's row split against a block of queries with ONE bf16 MFMA per product
+// (v_mfma_f32_32x32x16_bf16, fp32 accumulation) and keep, per (query, list), the KM best
+// approximate keys in registers; knn_refine.hip reranks and certifies the merged candidates.  It
+// replaces the arithmetic of faiss IndexFlat.search reached from main/search_from_image.py:247.
+//
+// Why a second kernel: the 128 x 128 tile of the generic kernel stages 2 bytes of LDS-DMA and
+// reads 1.25 KiB of LDS per MFMA; at one workgroup per CU a 256 x 256 tile halves the staged bytes
+// (2·N·D·Q·(1/BM + 1/BQ)) and a 128-row x 64-query wave tile reads 0.75 KiB per MFMA.
+//
+// Geometry: 8 waves = 2 (rows) x 4 (queries), wave tile 128 rows x 64 queries = 4 x 2 blocks of
+// 32 x 32.  Stage = 64 bf16 of depth per row (128 B): A 256 rows + B 256 queries = 64 KiB, two
+// stages in flight (128 KiB + row norms).  Each wave moves 8 one-KiB pieces per stage (waves 0-3
+// the corpus tile, 4-7 the query tile) with global_load_lds_dwordx4 in the saddr form: one
+// per-piece 32-bit lane offset fixed for the whole launch, one scalar base per stage.
+// Per stage: issue the next stage's DMA, four 16-deep k-steps (fragments of step c+1 read while
+// step c's 8 MFMAs run), wait for the own DMA, barrier.  After a tile's last stage: barrier,
+// top-k epilogue (keys parked in the just-consumed stage), barrier.
+//
+// LDS image: row r of a stage, 16-B chunk c stored at chunk c ^ ((r >> 1) & 7) (two 128-B rows
+// per 256-B bank row); the XOR is applied on the DMA's per-lane global source offset, so every
+// ds_read_b128 lane group of 16 hits 16 distinct bank slots.
+//
+// Accumulator map (v_mfma_f32_32x32x16_bf16): col = lane & 31 -> query, row = (reg & 3) +
+// 8 (reg >> 2) + 4 (lane >> 5) -> corpus row: each lane owns two queries (one per query block)
+// and 16 rows of each row block, so the top-k needs no data movement.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "knn_kernels.h"
+
+namespace imgrec {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kNW = 8;                    // waves: 2 along rows x 4 along queries
+constexpr int kBM = kB16BigRows;          // 256 corpus rows per tile
+constexpr int kBQ = kB16BigQueries;       // 256 queries per workgroup
+constexpr int kBKW = 32;                  // 32-bit words (2 bf16) per staged row
+constexpr int kRowB = kBKW * 4;           // 128 B
+constexpr int kSA = kBM * kRowB;          // A (corpus) stage bytes
+constexpr int kSB = kBQ * kRowB;          // B (query) stage bytes
+constexpr int kStage = kSA + kSB;         // 64 KiB
+constexpr int kNS = 2;
+constexpr int kLPW = (kBM + kBQ) / 8 / kNW;   // one-KiB pieces (8 rows x 128 B) per wave per stage
+constexpr int kNormOff = kNS * kStage;
+constexpr int kLDS = kNormOff + kNS * kBM * 4;
+static_assert(kLDS <= 160 * 1024, "LDS budget");
+static_assert(kLPW == 8, "dma8 issues eight pieces");
+static_assert(kNW * 16 * 64 * 4 <= kStage, "epilogue parking must fit in one stage");
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+// Eight one-KiB LDS-DMA pieces: LDS destinations lds0 + j KiB, global sources sbase + v[j] (bytes).
+// M0 is saved and restored inside the statement; hipcc sees no LDS write, so it inserts no wait
+// in front of later fragment reads — every wait on these is the explicit vmcnt below.
+__device__ __forceinline__ void dma8(const void* sbase, uint32_t lds0, const uint32_t (&v)[8]) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %10\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %2, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %3, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %4, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %5, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %6, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %7, %9\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %8, %9\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+          "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds0))
+        : "memory", "scc");
+}
+
+// One 4-byte-per-lane LDS-DMA (row norms of a tile).
+__device__ __forceinline__ void dma4_norm(const float* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+
+__device__ __forceinline__ void barrier_lds() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Ascending register list; labels arrive in increasing order per lane, so an equal key lands
+// behind the entries already present (ties by smaller label).
+template <int K>
+__device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float d, int id) {
+#pragma unroll
+    for (int p = K - 1; p > 0; --p) {
+        const bool shift = d < kd[p - 1];
+        const bool here = !shift && d < kd[p];
+        kd[p] = shift ? kd[p - 1] : (here ? d : kd[p]);
+        ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
+    }
+    const bool here0 = d < kd[0];
+    kd[0] = here0 ? d : kd[0];
+    ki[0] = here0 ? id : ki[0];
+}
+
+}  // namespace
+
+template <int KM, int L2>
+__global__ void __launch_bounds__(512, 2)
+knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ xnorm, int nrows,
+                    int dw, const uint32_t* __restrict__ qh, const float* __restrict__ qnorm, int nq,
+                    int ntiles, int nsplit, int nqb, int64_t id_offset, float* __restrict__ cand_d,
+                    int64_t* __restrict__ cand_i, int ncand) {
+    __shared__ __attribute__((aligned(16))) char smem[kLDS];
+
+    // XCD-aware bijective block -> (query block, row split) map (as knn_tile_topk_kernel): the
+    // query blocks of one row split run on one XCD and share its L2 for the corpus tiles.
+    const int nwg = gridDim.x, wg = blockIdx.x;
+    const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
+    const int qb = wgid % nqb;
+    const int split = wgid / nqb;
+    const int t0 = (int)((int64_t)split * ntiles / nsplit);
+    const int t1 = (int)((int64_t)(split + 1) * ntiles / nsplit);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wr = wave >> 2, wq = wave & 3;
+    const int li = lane & 31, lh = lane >> 5;
+    int qcol[2];
+    qcol[0] = qb * kBQ + wq * 64 + li;
+    qcol[1] = qcol[0] + 32;
+    float qn[2] = {0.f, 0.f};
+    if (L2) { qn[0] = qnorm[qcol[0]]; qn[1] = qnorm[qcol[1]]; }
+    asm volatile("" : "+v"(qn[0]), "+v"(qn[1]));   // consume the loads before the DMA stream
+
+    // DMA pieces of this wave: 8 consecutive pieces of the A tile (waves 0-3) or B tile (4-7);
+    // lane -> (row prow of the piece, chunk pchk), source chunk pre-swizzled.
+    const bool isA = wave < 4;
+    const int pbase = (isA ? wave : wave - 4) * kLPW;          // first piece index in its tile
+    const int prow = lane >> 3, pchk = lane & 7;
+    uint32_t voff[kLPW];
+#pragma unroll
+    for (int j = 0; j < kLPW; ++j) {
+        const int r = (pbase + j) * 8 + prow;
+        voff[j] = (uint32_t)((r * dw + 4 * (pchk ^ ((r >> 1) & 7))) * 4);
+    }
+    const uint32_t smem0 = lds_u32(smem);
+    const uint32_t pdst = (uint32_t)((isA ? 0 : kSA) + pbase * 1024);
+
+    // fragment read offsets (bytes, inside a stage): k-step c of this lane half = logical chunk
+    // lh*4 + c of row li of each 32-row block
+    const int fsw = (li >> 1) & 7;
+    int aoff[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) aoff[c] = (wr * 128 + li) * kRowB + 16 * ((lh * 4 + c) ^ fsw);
+    const int boff = kSA + (wq * 64 - wr * 128) * kRowB;       // B fragment = A offset + boff
+
+    float kd[2][KM];
+    int ki[2][KM];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int p = 0; p < KM; ++p) { kd[h][p] = INFINITY; ki[h][p] = -1; }
+
+    const int nst = dw / kBKW;                                  // stages per tile
+    const int total = (t1 - t0) * nst;
+    const uint32_t* qblk = qh + (size_t)qb * kBQ * dw;
+
+    auto issue = [&](int g) __attribute__((always_inline)) {
+        const int it = t0 + g / nst, is = g - (g / nst) * nst;
+        const int buf = g & 1;
+        const uint32_t* src = (isA ? xh + (size_t)it * kBM * dw : qblk) + is * kBKW;
+        dma8(src, smem0 + (uint32_t)(buf * kStage) + pdst, voff);
+        if (is == 0 && wave < 4)                                // the tile's 256 row norms
+            dma4_norm(xnorm + (size_t)it * kBM + wave * 64 + lane,
+                      smem0 + (uint32_t)(kNormOff + ((it - t0) & 1) * kBM * 4 + wave * 256));
+    };
+
+    if (total > 0) {
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+    }
+
+    int g = 0;
+    for (int t = t0; t < t1; ++t) {
+        const int row0 = t * kBM;
+        f32x16 acc[4][2];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[rb][h] = (f32x16){0.f};
+
+        int buf = 0;
+        for (int s = 0; s < nst; ++s, ++g) {
+            buf = g & 1;
+            if (g + 1 < total) issue(g + 1);                    // into the buffer read last stage
+            const char* sb = smem + buf * kStage;
+            u32x4 fa[2][4], fb[2][2];
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+                fa[0][rb] = *reinterpret_cast<const u32x4*>(sb + aoff[0] + rb * 32 * kRowB);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                fb[0][h] = *reinterpret_cast<const u32x4*>(sb + aoff[0] + boff + h * 32 * kRowB);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int cur = c & 1, nxt = cur ^ 1;
+                if (c < 3) {
+#pragma unroll
+                    for (int rb = 0; rb < 4; ++rb)
+                        fa[nxt][rb] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + rb * 32 * kRowB);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        fb[nxt][h] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + boff + h * 32 * kRowB);
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int rb = 0; rb < 4; ++rb)
+                        acc[rb][h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            __builtin_bit_cast(bf16x8, fa[cur][rb]), __builtin_bit_cast(bf16x8, fb[cur][h]),
+                            acc[rb][h], 0, 0, 0);
+            }
+            // own DMA of the next stage landed, own fragment reads done; then everyone's
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if (s + 1 < nst) barrier_lds();
+        }
+
+        // ---- epilogue: every wave's fragment reads of the spent stage `buf` are done after this
+        // barrier; keys are parked there (the next DMA into `buf` is issued after the next one).
+        barrier_lds();
+        const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) & 1) * kBM * 4);
+        float* park = reinterpret_cast<float*>(smem + buf * kStage) + wave * (16 * 64);
+        const bool full = row0 + kBM <= nrows;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (qcol[h] >= nq) continue;
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb) {
+                const float tau = kd[h][KM - 1];
+                const float tau_p = __shfl_xor(tau, 32, 64);   // partner lane: same query
+                const int rbase = wr * 128 + rb * 32 + 4 * lh;  // tile row of accumulator reg 0
+                float key[16];
+                unsigned mask = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (L2) n4 = *reinterpret_cast<const float4*>(nrm + rbase + 8 * j);
+                    const float nv[4] = {n4.x, n4.y, n4.z, n4.w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 4 * j + i;
+                        float kv;
+                        if (L2) {
+                            kv = fmaf(-2.f, acc[rb][h][r], qn[h] + nv[i]);
+                            kv = kv < 0.f ? 0.f : kv;
+                        } else {
+                            kv = -acc[rb][h][r];
+                        }
+                        key[r] = kv;
+                        const bool pass = (full || row0 + rbase + 8 * j + i < nrows) && kv < tau &&
+                                          kv <= tau_p;
+                        mask |= (unsigned)pass << r;
+                    }
+                }
+                if (__any(mask != 0)) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) park[r * 64 + lane] = key[r];
+                    unsigned m = mask;
+                    while (__any(m != 0)) {
+                        if (m) {
+                            const int r = __builtin_ctz(m);
+                            m &= m - 1u;
+                            const float kv = park[r * 64 + lane];
+                            const int row = row0 + rbase + (r & 3) + 8 * (r >> 2);
+                            if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, row);
+                        }
+                    }
+                }
+            }
+        }
+        barrier_lds();                                          // parking done before refill
+    }
+
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (qcol[h] >= nq) continue;
+        const size_t base = (size_t)qcol[h] * ncand + (size_t)((split * 2 + wr) * 2 + lh) * KM;
+#pragma unroll
+        for (int p = 0; p < KM; ++p) {
+            cand_d[base + p] = kd[h][p];
+            cand_i[base + p] = ki[h][p] < 0 ? (int64_t)-1 : (int64_t)ki[h][p] + id_offset;
+        }
+    }
+}
+
+hipError_t launch_b16_big(const TileArgs& a, hipStream_t st) {
+    if (a.wr != 2 || a.wq != 4 || a.dp % kBKW != 0) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(kNW * 64);
+    const uint32_t* xh = reinterpret_cast<const uint32_t*>(a.xb);
+    const uint32_t* qh = reinterpret_cast<const uint32_t*>(a.qp);
+#define IMGREC_LAUNCH_B16(KMV, L2V)                                                                \
+    hipLaunchKernelGGL((knn_b16_tile_kernel<KMV, L2V>), grid, block, 0, st, xh, a.xnorm, a.nrows,  \
+                       a.dp, qh, a.qnorm, a.nq, a.ntiles, a.nsplit, a.nqb, a.id_offset, a.cand_d,   \
+                       a.cand_i, a.ncand)
+    if (a.km == 8) {
+        if (a.metric == 1) IMGREC_LAUNCH_B16(8, 1); else IMGREC_LAUNCH_B16(8, 0);
+    } else if (a.km == 10) {
+        if (a.metric == 1) IMGREC_LAUNCH_B16(10, 1); else IMGREC_LAUNCH_B16(10, 0);
+    } else {
+        return hipErrorInvalidValue;
+    }
+#undef IMGREC_LAUNCH_B16
+    return hipGetLastError();
+}
+
+}  // namespace imgrec

@@ -76,6 +76,7 @@ int grow(T** p, size_t* cap, size_t need) {
 struct Plan {
     int wr, wq, km, bm, bq;
     int nqb, nq_pad, ntiles, nsplit, ncand, wgs;
+    bool big;                    // bf16 path: the 256 x 256-tile kernel (knn_b16.hip)
 };
 
 // Fused-kernel geometry for one query chunk (see DESIGN.md "Launch plan").
@@ -160,10 +161,26 @@ inline float b16_acc_coef(int dpb) {
 constexpr int kB16Cand = 64;
 inline int b16_km(int k) { return k <= 16 ? 16 : 32; }
 
-// bf16-path geometry: (kB16WR, kB16WQ) workgroups, kB16WGPCU per CU.
-Plan make_b16_plan(int64_t ntotal, int64_t nq, int km, int cus) {
+// bf16-path geometry: large batches with k <= 10 on the 256 x 256-tile kernel (one workgroup
+// per CU, lane lists of 8 / 10); otherwise (kB16WR, kB16WQ) workgroups, kB16WGPCU per CU.
+Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus) {
     Plan p{};
-    p.km = km;
+    if (nq >= imgrec::kB16BigMinQ && k <= 10) {
+        p.big = true;
+        p.km = k <= 8 ? 8 : 10;
+        p.wr = 2;
+        p.wq = 4;
+        p.bm = imgrec::kB16BigRows;
+        p.bq = imgrec::kB16BigQueries;
+        p.nqb = (int)((nq + p.bq - 1) / p.bq);
+        p.nq_pad = p.nqb * p.bq;
+        p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+        p.nsplit = std::max(1, std::min((cus + p.nqb - 1) / p.nqb, p.ntiles));
+        p.ncand = p.nsplit * p.wr * 2 * p.km;
+        p.wgs = p.nqb * p.nsplit;
+        return p;
+    }
+    p.km = b16_km(k);
     p.wr = imgrec::kB16WR;
     p.wq = imgrec::kB16WQ;
     p.bm = p.wr * 32 * imgrec::kB16WB;
@@ -412,8 +429,9 @@ int cascade(knn_index* ix, const float* qpad, const float* qnorm, const int* lis
 int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
               int64_t* I, hipStream_t st, bool timed) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
-    const int km = b16_km(k), kc = kB16Cand;
-    const Plan p = make_b16_plan(ix->ntotal, nq, km, ix->cus);
+    const int kc = kB16Cand;
+    const Plan p = make_b16_plan(ix->ntotal, nq, k, ix->cus);
+    const int km = p.km;
     int rc;
     if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
     if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)p.nq_pad * ix->dpb)) != KNN_OK) return rc;
@@ -434,7 +452,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand;
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
-    KNN_HIP(imgrec::launch_tile_topk(a, st));
+    KNN_HIP(p.big ? imgrec::launch_b16_big(a, st) : imgrec::launch_tile_topk(a, st));
     if (e1) KNN_HIP(hipEventRecord(e1, st));
     KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, p.ncand / km, km, p.ncand,
                                             km, kc, ix->cand2_d, ix->cand2_i, ix->floor, st));
@@ -541,7 +559,7 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         const bool b16 = use_b16(ix, cn, k);
         const bool split = !b16 && use_split(ix, cn, k);
         // padding: the query tile of the plan this chunk will run
-        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, b16_km(k), ix->cus)
+        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus)
                      : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                              : make_plan(ix->ntotal, cn, k, ix->cus);
         const int64_t nq_pad = p.nq_pad;
@@ -832,7 +850,7 @@ int knn_last_path(const knn_index_t* ix) { return ix ? ix->last_path : KNN_EINVA
 int knn_plan(const knn_index_t* ix, int64_t nq, int k, int* tr, int* tq, int* splits, int* wgs) {
     if (!ix || !tr || !tq || !splits || !wgs) KNN_FAIL(KNN_EINVAL, "NULL argument");
     const int64_t cn = std::min(nq, kQueryChunk);
-    const Plan p = use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, b16_km(k), ix->cus)
+    const Plan p = use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, k, ix->cus)
                  : use_split(ix, cn, k) ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                                         : make_plan(ix->ntotal, cn, k, ix->cus);
     *tr = p.bm;

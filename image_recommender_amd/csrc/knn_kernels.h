@@ -96,9 +96,17 @@ constexpr int kSplitBK = IMGREC_SPLIT_BK, kSplitNS = IMGREC_SPLIT_NS, kSplitWB =
 constexpr int kB16WR = IMGREC_B16_WR, kB16WQ = IMGREC_B16_WQ, kB16WB = IMGREC_B16_WB;
 constexpr int kB16NS = IMGREC_B16_NS, kB16WGPCU = IMGREC_B16_WGPCU, kB16Pad = 64;
 
+// 256 x 256-tile bf16 kernel (knn_b16.hip): one 8-wave workgroup per CU, k <= 10, batches of at
+// least kB16BigMinQ queries.
+#ifndef IMGREC_B16_BIG_MINQ
+#define IMGREC_B16_BIG_MINQ 512
+#endif
+constexpr int kB16BigRows = 256, kB16BigQueries = 256, kB16BigMinQ = IMGREC_B16_BIG_MINQ;
+
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st);
+hipError_t launch_b16_big(const TileArgs& a, hipStream_t st);     // knn_b16.hip
 hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st);

@@ -197,3 +197,45 @@ def test_bf16_mode_rejected_for_tiny_d(faiss):
         idx.search_mode = "bf16"
     with pytest.raises(ValueError):
         idx.search_mode = "fp8"
+
+
+@pytest.mark.parametrize("n,d,nq,k,metric", [
+    (20000, 1968, 600, 10, "l2"),     # config-3 width, two query blocks (second one partial)
+    (5000, 100, 1100, 8, "ip"),       # narrow rows (2 stages per tile), five query blocks
+    (777, 256, 513, 1, "l2"),         # tiny corpus: partial last tile, splits of one tile
+    (30000, 768, 1024, 10, "cosine"),
+    (40000, 512, 1024, 5, "l2"),
+])
+def test_bf16_big_tile_kernel(faiss, n, d, nq, k, metric):
+    """Batches of >= 512 queries with k <= 10 run the 256 x 256-tile kernel (knn_b16.hip)."""
+    if d == 1968:
+        xb = concat_rows(n, seed=n)
+        xq = xb[:nq] + np.float32(0.01)
+    else:
+        xb = mixture(n, d, centres=70, seed=n + d)
+        xq = mixture(nq, d, centres=70, seed=n + d + 1)
+    idx = _index(faiss, d, metric)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, k)
+    assert idx.search_stats()[0] == nq
+    _bound_holds(idx)
+    sel = np.arange(0, nq, 7)                  # the oracle check on a subsample keeps it fast
+    check_knn(D[sel], I[sel], xb, xq[sel], k, metric, min_exact_frac=0.5)
+    idx.search_mode = "exact"
+    De, Ie = idx.search(xq, k)
+    assert (I == Ie).mean() > 0.97
+
+
+def test_bf16_big_tile_self_query_concat(faiss):
+    xb = concat_rows(50000, seed=17)
+    q = xb[:1024].copy()
+    faiss.normalize_L2(q)
+    idx = faiss.IndexFlatL2(xb.shape[1])
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(q, 10)
+    ncand, nfb = idx.search_stats()
+    assert ncand == 1024 and nfb <= 100
+    assert (I[:, 0] == np.arange(1024)).all()
+    np.testing.assert_allclose(D[:, 0], 4 - 2 * np.sqrt(3), rtol=0, atol=1e-5)
