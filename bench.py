@@ -180,14 +180,23 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
     }
 
 
-def pmc_traffic(wr: int, wq: int, path: int):
+def kernel_pattern(tile_rows: int, tile_queries: int, path: int, k: int):
+    """(display name, regex) of the fused kernel a search ran: knn_b16_tile_kernel<KM, L2> for the
+    256 x 256-tile bf16 kernel, else knn_tile_topk_kernel<WR, WQ, KM, NS, BK, MODE, WB> (MODE 0
+    fp32, 1 split, 2 bf16)."""
+    if path == 2 and tile_rows == 256 and tile_queries == 256:
+        return f"knn_b16_tile_kernel<{8 if k <= 8 else 10}, 1>", r"knn_b16_tile_kernel<\d+, 1>"
+    wr, wq = tile_rows // 128, tile_queries // 32
+    return (f"knn_tile_topk_kernel<{wr}, {wq}, ..., mode {path}>",
+            rf"knn_tile_topk_kernel<{wr}, {wq}, \d+, \d+, \d+, {path}, \d+>")
+
+
+def pmc_traffic(pattern: str):
     """HBM bytes per launch of the fused kernel from the newest profiles/*_traffic.json written by
-    tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None.
-    Kernel names are knn_tile_topk_kernel<WR, WQ, KM, NS, BK, MODE, WB> (MODE 0 fp32, 1 split,
-    2 bf16)."""
+    tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None."""
     import glob
     import re
-    pat = re.compile(rf"knn_tile_topk_kernel<{wr}, {wq}, \d+, \d+, \d+, {path}, \d+>")
+    pat = re.compile(pattern)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
     for f in reversed(files):
         try:
@@ -312,7 +321,8 @@ def main():
         n_local = shard.local_rows
         flops = 2.0 * n_local * D_total * a.nq
         split = split_q > 0
-        traffic = pmc_traffic(tr.value // 128, tq.value // 32, path) if world == 1 else None
+        kname, kpat = kernel_pattern(tr.value, tq.value, path, a.k)
+        traffic = pmc_traffic(kpat) if world == 1 else None
         achieved = flops / (kern_ms * 1e-3) / 1e12
         # matrix-pipe ceiling for the algorithmic 2NDQ flop: bf16 path one bf16 MFMA per product
         # (bf16 dense peak); split path three (hi.hi + hi.lo + lo.hi: bf16 peak / 3); exact path
@@ -358,7 +368,7 @@ def main():
                 "peak_basis": peak_basis,
                 "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None,
-                "kernel": f"knn_tile_topk_kernel<{tr.value // 128},{tq.value // 32},...,mode {path}>",
+                "kernel": kname,
                 "kernel_ms": kern_ms,
                 "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
             },

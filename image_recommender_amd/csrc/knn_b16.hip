@@ -14,9 +14,11 @@
 // 32 x 32.  Stage = 64 bf16 of depth per row (128 B): A 256 rows + B 256 queries = 64 KiB, two
 // stages in flight (128 KiB + row norms).  Each wave moves 8 one-KiB pieces per stage (waves 0-3
 // the corpus tile, 4-7 the query tile) with global_load_lds_dwordx4 in the saddr form: one
-// per-piece 32-bit lane offset fixed for the whole launch, one scalar base per stage.
-// Per stage: issue the next stage's DMA, four 16-deep k-steps (fragments of step c+1 read while
-// step c's 8 MFMAs run), wait for the own DMA, barrier.  After a tile's last stage: barrier,
+// per-piece 32-bit lane offset fixed for the whole launch, one scalar base per stage, one M0 write
+// per four pieces (instruction offsets).  Per stage: issue the next stage's DMA, four 16-deep
+// k-steps (fragments of step c+1 read while step c's 8 MFMAs run), wait for the own DMA, barrier.
+// Measured bound: the per-CU global->LDS rate (~25 B/clk; 64 KiB per stage against 2048 MFMA
+// cycles per SIMD) — spreading the DMA issue between k-steps did not help.  After a tile's last stage: barrier,
 // top-k epilogue (keys parked in the just-consumed stage), barrier.
 //
 // LDS image: row r of a stage, 16-B chunk c stored at chunk c ^ ((r >> 1) & 7) (two 128-B rows
@@ -32,6 +34,10 @@
 #include <math.h>
 
 #include "knn_kernels.h"
+
+#ifndef IMGREC_B16_DMA_SPREAD      // 1: DMA halves between k-steps 0/1 (measured slower: 4.48
+#define IMGREC_B16_DMA_SPREAD 0    //    vs 4.25 ms); 0: both halves at the stage start
+#endif
 
 namespace imgrec {
 namespace {
@@ -53,41 +59,29 @@ constexpr int kLPW = (kBM + kBQ) / 8 / kNW;   // one-KiB pieces (8 rows x 128 B)
 constexpr int kNormOff = kNS * kStage;
 constexpr int kLDS = kNormOff + kNS * kBM * 4;
 static_assert(kLDS <= 160 * 1024, "LDS budget");
-static_assert(kLPW == 8, "dma8 issues eight pieces");
+static_assert(kLPW == 8, "two dma4x halves of four pieces");
 static_assert(kNW * 16 * 64 * 4 <= kStage, "epilogue parking must fit in one stage");
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
     return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
 
-// Eight one-KiB LDS-DMA pieces: LDS destinations lds0 + j KiB, global sources sbase + v[j] (bytes).
-// M0 is saved and restored inside the statement; hipcc sees no LDS write, so it inserts no wait
-// in front of later fragment reads — every wait on these is the explicit vmcnt below.
-__device__ __forceinline__ void dma8(const void* sbase, uint32_t lds0, const uint32_t (&v)[8]) {
+// Four one-KiB LDS-DMA pieces under ONE M0 value: the instruction offset (j KiB) moves both the
+// global source and the LDS destination (measured, tools/micro/glds_offset.hip), so the per-lane
+// offsets v[j] are pre-reduced by j KiB.
+__device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, const uint32_t (&v)[8], int h) {
     unsigned keep;
     asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %10\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %2, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %3, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %4, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %5, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %6, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %7, %9\n\t"
-        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %8, %9\n\t"
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %5\n\t"
+        "global_load_lds_dwordx4 %2, %5 offset:1024\n\t"
+        "global_load_lds_dwordx4 %3, %5 offset:2048\n\t"
+        "global_load_lds_dwordx4 %4, %5 offset:3072\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
-          "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds0))
-        : "memory", "scc");
+        : "v"(v[4 * h]), "v"(v[4 * h + 1]), "v"(v[4 * h + 2]), "v"(v[4 * h + 3]), "s"(sbase),
+          "s"(__builtin_amdgcn_readfirstlane(lds0))
+        : "memory");
 }
 
 // One 4-byte-per-lane LDS-DMA (row norms of a tile).
@@ -116,6 +110,26 @@ __device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float 
         ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
     }
     const bool here0 = d < kd[0];
+    kd[0] = here0 ? d : kd[0];
+    ki[0] = here0 ? id : ki[0];
+}
+
+// (d1, i1) ranks before (d2, i2): smaller key, ties by smaller label (empty = label -1 last).
+__device__ __forceinline__ bool rank_lt(float d1, int i1, float d2, int i2) {
+    return i2 < 0 || d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+// Insert into an ascending list when labels arrive in any order (the end-of-kernel folds).
+template <int K>
+__device__ __forceinline__ void insert_any(float (&kd)[K], int (&ki)[K], float d, int id) {
+#pragma unroll
+    for (int p = K - 1; p > 0; --p) {
+        const bool shift = rank_lt(d, id, kd[p - 1], ki[p - 1]);
+        const bool here = !shift && rank_lt(d, id, kd[p], ki[p]);
+        kd[p] = shift ? kd[p - 1] : (here ? d : kd[p]);
+        ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
+    }
+    const bool here0 = rank_lt(d, id, kd[0], ki[0]);
     kd[0] = here0 ? d : kd[0];
     ki[0] = here0 ? id : ki[0];
 }
@@ -160,7 +174,8 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 #pragma unroll
     for (int j = 0; j < kLPW; ++j) {
         const int r = (pbase + j) * 8 + prow;
-        voff[j] = (uint32_t)((r * dw + 4 * (pchk ^ ((r >> 1) & 7))) * 4);
+        // minus the instruction offset dma4x adds to piece j (>= 0: row r >= 8j, dw >= 32)
+        voff[j] = (uint32_t)((r * dw + 4 * (pchk ^ ((r >> 1) & 7))) * 4 - 1024 * (j & 3));
     }
     const uint32_t smem0 = lds_u32(smem);
     const uint32_t pdst = (uint32_t)((isA ? 0 : kSA) + pbase * 1024);
@@ -184,18 +199,20 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int total = (t1 - t0) * nst;
     const uint32_t* qblk = qh + (size_t)qb * kBQ * dw;
 
-    auto issue = [&](int g) __attribute__((always_inline)) {
+    // DMA of stage g, half h (pieces 4h..4h+3; half 0 also the tile's row norms)
+    auto issue_half = [&](int g, int h) __attribute__((always_inline)) {
         const int it = t0 + g / nst, is = g - (g / nst) * nst;
         const int buf = g & 1;
         const uint32_t* src = (isA ? xh + (size_t)it * kBM * dw : qblk) + is * kBKW;
-        dma8(src, smem0 + (uint32_t)(buf * kStage) + pdst, voff);
-        if (is == 0 && wave < 4)                                // the tile's 256 row norms
+        dma4x(src, smem0 + (uint32_t)(buf * kStage) + pdst + 4096u * h, voff, h);
+        if (h == 0 && is == 0 && wave < 4)                      // the tile's 256 row norms
             dma4_norm(xnorm + (size_t)it * kBM + wave * 64 + lane,
                       smem0 + (uint32_t)(kNormOff + ((it - t0) & 1) * kBM * 4 + wave * 256));
     };
 
     if (total > 0) {
-        issue(0);
+        issue_half(0, 0);
+        issue_half(0, 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();
     }
@@ -212,7 +229,16 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         int buf = 0;
         for (int s = 0; s < nst; ++s, ++g) {
             buf = g & 1;
-            if (g + 1 < total) issue(g + 1);                    // into the buffer read last stage
+            // the next stage's DMA goes into the buffer read last stage, in two halves placed
+            // between k-steps (issue cost hides behind the MFMAs already queued)
+#ifdef IMGREC_ABLATE_NO_DMA
+            const bool dma_next = g + 1 < total && s == 0;      // ablation: norms + one stage per tile
+#else
+            const bool dma_next = g + 1 < total;
+#endif
+#if !IMGREC_B16_DMA_SPREAD
+            if (dma_next) { issue_half(g + 1, 0); issue_half(g + 1, 1); }
+#endif
             const char* sb = smem + buf * kStage;
             u32x4 fa[2][4], fb[2][2];
 #pragma unroll
@@ -232,6 +258,13 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     for (int h = 0; h < 2; ++h)
                         fb[nxt][h] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + boff + h * 32 * kRowB);
                 }
+#if IMGREC_B16_DMA_SPREAD
+                if (c < 2) {                                    // half c between k-steps (A/B knob)
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (dma_next) issue_half(g + 1, c);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#endif
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -241,7 +274,11 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                             acc[rb][h], 0, 0, 0);
             }
             // own DMA of the next stage landed, own fragment reads done; then everyone's
+#ifdef IMGREC_ABLATE_NO_WAIT
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
             if (s + 1 < nst) barrier_lds();
         }
 
@@ -253,7 +290,11 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         const bool full = row0 + kBM <= nrows;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+#ifdef IMGREC_ABLATE_NO_EPILOGUE
+            if (qcol[h] >= nq || row0 >= 0) continue;          // ablation: keeps acc live only
+#else
             if (qcol[h] >= nq) continue;
+#endif
 #pragma unroll
             for (int rb = 0; rb < 4; ++rb) {
                 const float tau = kd[h][KM - 1];
@@ -301,10 +342,43 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         barrier_lds();                                          // parking done before refill
     }
 
+    // ---- one list per (query, row split): fold the partner lane's list (lane ^ 32, the query's
+    // other rows) by shuffles, then wave wr = 1's lists into wave wr = 0's through LDS.  Entries a
+    // fold drops rank behind the folded list's last entry, which the merge floor covers.
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int p = 0; p < KM; ++p) {
+            const float od = __shfl_xor(kd[h][p], 32, 64);
+            const int oi = __shfl_xor(ki[h][p], 32, 64);
+            if (lh == 0 && oi >= 0 && rank_lt(od, oi, kd[h][KM - 1], ki[h][KM - 1]))
+                insert_any<KM>(kd[h], ki[h], od, oi);
+        }
+    }
+    float* xd = reinterpret_cast<float*>(smem);                 // [wq][h][li][KM] keys, then labels
+    int* xi = reinterpret_cast<int*>(smem) + 4 * 2 * 32 * KM;
+    if (wr == 1 && lh == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int p = 0; p < KM; ++p) {
+                xd[((wq * 2 + h) * 32 + li) * KM + p] = kd[h][p];
+                xi[((wq * 2 + h) * 32 + li) * KM + p] = ki[h][p];
+            }
+    }
+    __syncthreads();
+    if (wr == 1 || lh == 1) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int p = 0; p < KM; ++p) {
+            const float od = xd[((wq * 2 + h) * 32 + li) * KM + p];
+            const int oi = xi[((wq * 2 + h) * 32 + li) * KM + p];
+            if (oi >= 0 && rank_lt(od, oi, kd[h][KM - 1], ki[h][KM - 1]))
+                insert_any<KM>(kd[h], ki[h], od, oi);
+        }
         if (qcol[h] >= nq) continue;
-        const size_t base = (size_t)qcol[h] * ncand + (size_t)((split * 2 + wr) * 2 + lh) * KM;
+        const size_t base = (size_t)qcol[h] * ncand + (size_t)split * KM;
 #pragma unroll
         for (int p = 0; p < KM; ++p) {
             cand_d[base + p] = kd[h][p];

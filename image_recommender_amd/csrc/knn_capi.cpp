@@ -176,7 +176,7 @@ Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus) {
         p.nq_pad = p.nqb * p.bq;
         p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
         p.nsplit = std::max(1, std::min((cus + p.nqb - 1) / p.nqb, p.ntiles));
-        p.ncand = p.nsplit * p.wr * 2 * p.km;
+        p.ncand = p.nsplit * p.km;               // lists folded to one per (query, split)
         p.wgs = p.nqb * p.nsplit;
         return p;
     }
@@ -427,7 +427,7 @@ int cascade(knn_index* ix, const float* qpad, const float* qnorm, const int* lis
 // bf16 candidates (one bf16 MFMA per product) + exact fp32 rerank of K' = 64 + certificate;
 // uncertified queries cascade to the split path / exact kernel.
 int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
-              int64_t* I, hipStream_t st, bool timed) {
+              int64_t* I, hipStream_t st, bool timed, bool q_ready) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = kB16Cand;
     const Plan p = make_b16_plan(ix->ntotal, nq, k, ix->cus);
@@ -443,7 +443,8 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 1)) != KNN_OK) return rc;
     if ((rc = grow(&ix->err_ratio, &ix->err_ratio_cap, 1)) != KNN_OK) return rc;
-    KNN_HIP(imgrec::launch_bf16_rows(qpad, p.nq_pad, ix->dp, ix->dpb, ix->qb16, ix->q_resid, st));
+    if (!q_ready)   // else search_locked's fused query prep already wrote qb16 / q_resid
+        KNN_HIP(imgrec::launch_bf16_rows(qpad, p.nq_pad, ix->dp, ix->dpb, ix->qb16, ix->q_resid, st));
     TileArgs a{};
     a.wr = p.wr; a.wq = p.wq; a.km = km; a.wb = imgrec::kB16WB; a.mode = imgrec::kModeBF16;
     a.xb = reinterpret_cast<const float*>(ix->xh); a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
@@ -455,7 +456,8 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     KNN_HIP(p.big ? imgrec::launch_b16_big(a, st) : imgrec::launch_tile_topk(a, st));
     if (e1) KNN_HIP(hipEventRecord(e1, st));
     KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, p.ncand / km, km, p.ncand,
-                                            km, kc, ix->cand2_d, ix->cand2_i, ix->floor, st));
+                                            km, kc, ix->id_offset, ix->cand2_d, ix->cand2_i,
+                                            ix->floor, st));
     KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
     KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
     imgrec::RerankArgs r{};
@@ -567,9 +569,19 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         if (c0 == 0) ix->last_path = b16 ? 2 : (split ? 1 : 0);
         if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;
-        KNN_HIP(imgrec::launch_rows_ingest(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
-                                           ix->qpad, ix->qnorm, st));
-        rc = b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true)
+        bool q_ready = false;
+        if (b16 && ix->dpb <= 4096) {   // fused query prep: fp32 padded rows + norms + bf16 + residuals
+            if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)nq_pad * ix->dpb)) != KNN_OK) return rc;
+            if ((rc = grow(&ix->q_resid, &ix->q_resid_cap, (size_t)nq_pad)) != KNN_OK) return rc;
+            KNN_HIP(imgrec::launch_query_prep_b16(q + c0 * ix->d, cn, ix->d, ix->dp, ix->dpb, nq_pad,
+                                                  normalize, ix->qpad, ix->qnorm, ix->qb16,
+                                                  ix->q_resid, st));
+            q_ready = true;
+        } else {
+            KNN_HIP(imgrec::launch_rows_ingest(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
+                                               ix->qpad, ix->qnorm, st));
+        }
+        rc = b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true, q_ready)
              : split ? split_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true)
                      : exact_chunk(ix, ix->qpad, ix->qnorm, cn, k, D + c0 * k, I + c0 * k, st, true);
         if (rc != KNN_OK) return rc;

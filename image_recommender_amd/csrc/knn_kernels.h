@@ -115,7 +115,8 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
 // own lane lists can have (+inf when nothing was dropped).
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,
-                                   float* D, int64_t* I, float* floor, hipStream_t st);
+                                   int64_t id_offset, float* D, int64_t* I, float* floor,
+                                   hipStream_t st);
 hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStream_t st);
 
 hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32_t* dst,
@@ -128,6 +129,11 @@ hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int*
 // fp32 rows (stride dp) -> bf16 rows (stride dpb elements, zero padded), |x - bf16(x)| per row
 hipError_t launch_bf16_rows(const float* src, int64_t n, int dp, int dpb, uint16_t* dst,
                             float* resid, hipStream_t st);
+// bf16 path query side in one pass: padded fp32 rows + |q|^2 + bf16 rows + residual norms
+// (dpb <= 4096; hipErrorInvalidValue otherwise, the caller then uses the two kernels above)
+hipError_t launch_query_prep_b16(const float* src, int64_t n, int d, int dp, int dpb, int64_t n_pad,
+                                 int normalize, float* dst, float* norms, uint16_t* qb, float* resid,
+                                 hipStream_t st);
 hipError_t launch_max_norm(const float* xn, int64_t n, float* out, hipStream_t st);
 
 }  // namespace imgrec

@@ -723,14 +723,87 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
     return hipGetLastError();
 }
 
+// Candidate merge when every lane holds at most one sorted input list (<= 64 lists per query):
+// no insertion, the lane's list is its queue.  Entries are packed into one 64-bit value
+// (order-preserving key bits | local row), so each of the kout rounds is a 6-step u64 min
+// butterfly; the winning lane (unique: a row sits in one list) pops its head.
+__device__ __forceinline__ uint32_t key_bits_ordered(float k) {
+    const uint32_t u = __float_as_uint(k);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_from_ordered(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+template <int KIN>
+__global__ void __launch_bounds__(256)
+cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
+                       int nlists, int64_t stride_q, int64_t stride_l, int kout, int64_t id_offset,
+                       float* __restrict__ D, int64_t* __restrict__ I, float* __restrict__ floor_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;                                        // whole wave
+    constexpr uint64_t kEmpty = ~0ull;
+    uint64_t v[KIN];
+    float fl = INFINITY;
+    if (lane < nlists) {
+        const float* lp = cd + q * stride_q + (int64_t)lane * stride_l;
+        const int64_t* ip = ci + q * stride_q + (int64_t)lane * stride_l;
+#pragma unroll
+        for (int p = 0; p < KIN; ++p) {
+            const float kv = lp[p];
+            const int64_t lab = ip[p];
+            v[p] = lab < 0 ? kEmpty
+                           : ((uint64_t)key_bits_ordered(kv) << 32) | (uint32_t)(lab - id_offset);
+        }
+        if (ip[KIN - 1] >= 0) fl = lp[KIN - 1];                 // a full list: its last key
+    } else {
+#pragma unroll
+        for (int p = 0; p < KIN; ++p) v[p] = kEmpty;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+    if (lane == 0) floor_out[q] = fl;
+    for (int r = 0; r < kout; ++r) {
+        uint64_t b = v[0];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)b, off, 64);
+            const uint32_t hi = __shfl_xor((uint32_t)(b >> 32), off, 64);
+            const uint64_t o = ((uint64_t)hi << 32) | lo;
+            b = o < b ? o : b;
+        }
+        if (b != kEmpty && v[0] == b) {
+#pragma unroll
+            for (int p = 0; p < KIN - 1; ++p) v[p] = v[p + 1];
+            v[KIN - 1] = kEmpty;
+        }
+        if (lane == 0) {
+            D[q * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
+            I[q * kout + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b + id_offset;
+        }
+    }
+}
+
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,
-                                   float* D, int64_t* I, float* floor, hipStream_t st) {
+                                   int64_t id_offset, float* D, int64_t* I, float* floor,
+                                   hipStream_t st) {
     if (nq <= 0) return hipSuccess;
     if (kout <= 0 || kout > 64 || !floor) return hipErrorInvalidValue;
-    // one wave per query; the lane lists hold 32 entries (a lane's lists beyond that are covered
-    // by the floor), the output takes kout rounds of the wave argmin
-    hipLaunchKernelGGL((knn_merge_kernel<32, 1>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
+    if (nlists <= 64 && (kin == 8 || kin == 10 || kin == 16)) {
+        const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
+#define IMGREC_CAND_LANE(KV) hipLaunchKernelGGL((cand_merge_lane_kernel<KV>), grid, block, 0, st, cd, ci, \
+                                                nq, nlists, stride_q, stride_l, kout, id_offset, D, I, floor)
+        if (kin == 8) IMGREC_CAND_LANE(8);
+        else if (kin == 10) IMGREC_CAND_LANE(10);
+        else IMGREC_CAND_LANE(16);
+#undef IMGREC_CAND_LANE
+        return hipGetLastError();
+    }
+    // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is
+    // covered by the floor), the output takes kout rounds of the wave argmin
+    hipLaunchKernelGGL((knn_merge_kernel<16, 1>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
                        cd, ci, nq, nlists, kin, stride_q, stride_l, kout, 1, 0, D, I, floor);
     return hipGetLastError();
 }

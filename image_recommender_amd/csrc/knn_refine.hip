@@ -105,6 +105,86 @@ bf16_rows_kernel(const float* __restrict__ src, int64_t n, int dp, int dpb,
     if (lane == 0) resid[row] = sqrtf(acc);
 }
 
+// One wave per query row, the bf16 path's whole query side in one pass: raw row (d floats) ->
+// padded fp32 row (dp, zero tail; L2-normalised when `normalize`, faiss fvec_renorm_L2 scale), its
+// |q|^2, the bf16 row (dpb, RNE) and |q - bf16(q)|.  Rows n..n_pad-1 are zero.  Each lane holds
+// chunks of 8 elements (c = lane + 64 it) in registers; dpb <= 512 * IT.
+template <int IT>
+__global__ void __launch_bounds__(256)
+query_prep_b16_kernel(const float* __restrict__ src, int64_t n, int d, int dp, int dpb,
+                      int64_t n_pad, int normalize, float* __restrict__ dst,
+                      float* __restrict__ norms, uint16_t* __restrict__ qb,
+                      float* __restrict__ resid) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n_pad) return;
+    const bool real = row < n;
+    const float* s = src + row * d;
+    float e[IT][8];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int j0 = 8 * (lane + 64 * it);
+        if (real && (d & 3) == 0 && j0 + 8 <= d) {
+            const float4 v0 = *reinterpret_cast<const float4*>(s + j0);
+            const float4 v1 = *reinterpret_cast<const float4*>(s + j0 + 4);
+            e[it][0] = v0.x; e[it][1] = v0.y; e[it][2] = v0.z; e[it][3] = v0.w;
+            e[it][4] = v1.x; e[it][5] = v1.y; e[it][6] = v1.z; e[it][7] = v1.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) e[it][t] = (real && j0 + t < d) ? s[j0 + t] : 0.f;
+        }
+    }
+    float scale = 1.f;
+    if (normalize) {
+        float acc = 0.f;
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc = fmaf(e[it][t], e[it][t], acc);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (acc > 0.f) scale = (float)(1.0 / (double)sqrtf(acc));
+    }
+    float nacc = 0.f, racc = 0.f;
+    float* o = dst + row * dp;
+    uint16_t* ob = qb + row * dpb;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int c = lane + 64 * it;
+        if (8 * c >= dpb) continue;
+        float v[8];
+        uint32_t w[4];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            v[t] = normalize ? e[it][t] * scale : e[it][t];
+            nacc = fmaf(v[t], v[t], nacc);
+        }
+#pragma unroll
+        for (int p2 = 0; p2 < 4; ++p2) {
+            const uint32_t h0 = bf16_rne(v[2 * p2]), h1 = bf16_rne(v[2 * p2 + 1]);
+            const float r0 = v[2 * p2] - __uint_as_float(h0 << 16);
+            const float r1 = v[2 * p2 + 1] - __uint_as_float(h1 << 16);
+            racc = fmaf(r0, r0, racc);
+            racc = fmaf(r1, r1, racc);
+            w[p2] = h0 | (h1 << 16);
+        }
+        *reinterpret_cast<uint4*>(ob + 8 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (8 * c < dp) {                                    // dp is a multiple of 16
+            *reinterpret_cast<float4*>(o + 8 * c) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(o + 8 * c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        nacc += __shfl_xor(nacc, off, 64);
+        racc += __shfl_xor(racc, off, 64);
+    }
+    if (lane == 0) {
+        norms[row] = nacc;
+        resid[row] = sqrtf(racc);
+    }
+}
+
 template <typename I>
 __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
     return d1 < d2 || (d1 == d2 && i1 < i2);
@@ -122,75 +202,18 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
                       int* __restrict__ fail_list, float* __restrict__ err_ratio, int mode,
                       const float* __restrict__ q_resid, const float* __restrict__ xr_max,
                       const float* __restrict__ floor) {
+    // one 4-wave workgroup per query: every wave reranks a quarter of the prefix, wave 0 ranks
+    // and certifies
+    __shared__ float skey[64];
     const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
+    const int wave = threadIdx.x >> 6;
+    const int64_t q = blockIdx.x;
     const float* qv = qp + q * dp;
     const float qn = qnorm[q];
     const int64_t lab = lane < kc ? ci[q * kc + lane] : (int64_t)-1;
-    float key = INFINITY;
-
-    // exact fp32 keys, four candidates per pass (independent loads in flight)
-    const int n4 = dp / 4;
-    for (int c0 = 0; c0 < kc; c0 += 4) {
-        int64_t rows[4];
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int c = min(c0 + u, kc - 1);
-            const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
-            const int hi32 = __shfl((int)(lab >> 32), c, 64);
-            const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
-            rows[u] = (c0 + u < kc && l >= 0) ? l - id_offset : (int64_t)-1;
-        }
-        for (int i = lane; i < n4; i += 64) {
-            const float4 a = reinterpret_cast<const float4*>(qv)[i];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (rows[u] < 0) continue;
-                const float4 b = reinterpret_cast<const float4*>(xb + rows[u] * dp)[i];
-                acc[u] = fmaf(a.x, b.x, acc[u]);
-                acc[u] = fmaf(a.y, b.y, acc[u]);
-                acc[u] = fmaf(a.z, b.z, acc[u]);
-                acc[u] = fmaf(a.w, b.w, acc[u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) acc[u] += __shfl_xor(acc[u], off, 64);
-            if (rows[u] < 0 || lane != c0 + u) continue;
-            float kv;
-            if (metric == 1) {
-                kv = fmaf(-2.f, acc[u], qn + xn[rows[u]]);
-                kv = kv < 0.f ? 0.f : kv;
-            } else {
-                kv = -acc[u];
-            }
-            key = kv;
-        }
-    }
-
-    // rank of this lane's candidate among the valid ones by (key, label)
+    const float ak = lane < kc ? cd[q * kc + lane] : INFINITY;   // approximate key, ascending
     const bool valid = lab >= 0;
-    int rank = 0, nvalid = 0;
-    for (int i = 0; i < kc; ++i) {
-        const float ok = __shfl(key, i, 64);
-        const int lo32 = __shfl((int)(lab & 0xffffffff), i, 64);
-        const int hi32 = __shfl((int)(lab >> 32), i, 64);
-        const int64_t ol = ((int64_t)hi32 << 32) | (uint32_t)lo32;
-        if (ol < 0) continue;
-        ++nvalid;
-        if (valid && ranks_before_r(ok, ol, key, lab)) ++rank;
-    }
-    if (valid && rank < k) {
-        D[q * k + rank] = (metric == 1) ? key : -key;
-        I[q * k + rank] = lab;
-    }
-    if (lane >= nvalid && lane < k) {
-        D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
-        I[q * k + lane] = -1;
-    }
+    const int nvalid = __popcll(__ballot(valid));               // valid candidates come first
 
     const float xm = *xn_max;
     const float nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
@@ -214,25 +237,105 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
         return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
     };
 
-    // observed |approx - rerank| of every candidate relative to the two bounds (<= 1 whenever
-    // the bounds hold; reported by knn_search_stats so tests and the bench can watch it)
-    if (valid) {
-        const float ak = cd[q * kc + lane];
+    // Only a prefix of the (ascending) candidates can hold the answer: the k best by approximate
+    // key have exact keys <= a_k + E_a, so a candidate whose approximate key exceeds
+    // a_k + 2 (E_a + E_f) cannot rank before them.  The prefix P = {approx <= that} is reranked;
+    // the first candidate left out bounds every excluded candidate's approximate key from below.
+    int m = nvalid;
+    if (nvalid >= k) {
+        const float a_k = __shfl(ak, k - 1, 64);
+        const float thr = a_k + 2.02f * (bound_a(a_k) + bound_f(a_k));
+        m = __popcll(__ballot(valid && ak <= thr));
+    }
+
+    // exact fp32 keys of the prefix: candidate c goes to wave c % 4, four per wave pass
+    // (independent row loads in flight; each candidate's sum has the same order wherever it runs)
+    const int n4 = dp / 4;
+    const float4* q4 = reinterpret_cast<const float4*>(qv);
+    for (int c0 = wave; c0 < m; c0 += 16) {
+        const float4* r4[4];
+        float acc[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int c = min(c0 + 4 * v, m - 1);                // clamped: loads unconditional
+            const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
+            const int hi32 = __shfl((int)(lab >> 32), c, 64);
+            const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
+            r4[v] = reinterpret_cast<const float4*>(xb + (l - id_offset) * dp);
+            acc[v] = 0.f;
+        }
+#pragma unroll 4
+        for (int i = lane; i < n4; i += 64) {
+            const float4 a = q4[i];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float4 b = r4[v][i];
+                acc[v] = fmaf(a.x, b.x, acc[v]);
+                acc[v] = fmaf(a.y, b.y, acc[v]);
+                acc[v] = fmaf(a.z, b.z, acc[v]);
+                acc[v] = fmaf(a.w, b.w, acc[v]);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
+            const int c = c0 + 4 * v;
+            if (lane != c || c >= m) continue;                   // candidate c sits in lane c
+            float kv;
+            if (metric == 1) {
+                kv = fmaf(-2.f, acc[v], qn + xn[lab - id_offset]);
+                kv = kv < 0.f ? 0.f : kv;
+            } else {
+                kv = -acc[v];
+            }
+            skey[c] = kv;
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const float key = lane < m ? skey[lane] : INFINITY;
+
+    // rank of this lane's candidate inside the prefix by (key, label)
+    const bool inP = lane < m;
+    int rank = 0;
+    for (int i = 0; i < m; ++i) {
+        const float ok = __shfl(key, i, 64);
+        const int lo32 = __shfl((int)(lab & 0xffffffff), i, 64);
+        const int hi32 = __shfl((int)(lab >> 32), i, 64);
+        const int64_t ol = ((int64_t)hi32 << 32) | (uint32_t)lo32;
+        if (inP && ranks_before_r(ok, ol, key, lab)) ++rank;
+    }
+    if (inP && rank < k) {
+        D[q * k + rank] = (metric == 1) ? key : -key;
+        I[q * k + rank] = lab;
+    }
+    if (lane >= m && lane < k) {
+        D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
+        I[q * k + lane] = -1;
+    }
+
+    // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
+    // whenever the bounds hold; reported by knn_search_stats so tests and the bench can watch it)
+    if (inP) {
         const float r = fabsf(ak - key) / (bound_a(ak) + bound_f(key));
         atomicMax(reinterpret_cast<unsigned*>(err_ratio), __float_as_uint(r));
     }
 
-    // certificate: tau = smallest approximate key a row outside the candidates can have — the
-    // K'-th candidate's (when the set is full) and the merge floor (rows dropped by full lists);
-    // +inf means every row is a candidate
+    // certificate: tau = smallest approximate key a row outside the prefix can have — the K'-th
+    // candidate's (when the set is full), the merge floor (rows dropped by full lists) and the
+    // first candidate left out of the prefix; +inf means every row was reranked
     const int64_t lab_tau = ci[q * kc + kc - 1];
     float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
     if (floor) tau = fminf(tau, floor[q]);
+    const float a_out = __shfl(ak, min(m, 63), 64);
+    if (m < nvalid) tau = fminf(tau, a_out);
     if (tau == INFINITY) return;
-    float sk = (valid && rank == k - 1) ? key : -INFINITY;
+    float sk = (inP && rank == k - 1) ? key : -INFINITY;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
-    const bool certified = (tau - bound_a(tau)) > (sk + bound_f(sk));
+    // fewer than k reranked rows while rows were left out: nothing to certify with
+    const bool certified = m >= k && (tau - bound_a(tau)) > (sk + bound_f(sk));
     if (!certified && lane == 0) fail_list[atomicAdd(fail_count, 1)] = (int)q;
 }
 
@@ -291,7 +394,7 @@ hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
     if (a.kc > 64 || a.k > a.kc || a.dp % 4 != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rerank_certify_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, st,
+    hipLaunchKernelGGL(rerank_certify_kernel, dim3((unsigned)a.nq), dim3(256), 0, st,
                        a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci, a.kc,
                        a.nq, a.k, a.metric, a.c_split, a.c_fp, a.D, a.I, a.fail_count, a.fail_list,
                        a.err_ratio, a.mode, a.q_resid, a.xr_max, a.floor);
@@ -320,6 +423,23 @@ hipError_t launch_bf16_rows(const float* src, int64_t n, int dp, int dpb, uint16
     if (dpb % 8 != 0 || dp % 8 != 0 || dpb < dp) return hipErrorInvalidValue;
     hipLaunchKernelGGL(bf16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, src, n, dp,
                        dpb, dst, resid);
+    return hipGetLastError();
+}
+
+hipError_t launch_query_prep_b16(const float* src, int64_t n, int d, int dp, int dpb, int64_t n_pad,
+                                 int normalize, float* dst, float* norms, uint16_t* qb, float* resid,
+                                 hipStream_t st) {
+    if (n_pad <= 0) return hipSuccess;
+    if (dpb % 8 != 0 || dp % 16 != 0 || dpb < dp || dp < d) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((n_pad + 3) / 4)), block(256);
+#define IMGREC_QPREP(ITV) hipLaunchKernelGGL((query_prep_b16_kernel<ITV>), grid, block, 0, st, src, n, \
+                                             d, dp, dpb, n_pad, normalize, dst, norms, qb, resid)
+    if (dpb <= 512) IMGREC_QPREP(1);
+    else if (dpb <= 1024) IMGREC_QPREP(2);
+    else if (dpb <= 2048) IMGREC_QPREP(4);
+    else if (dpb <= 4096) IMGREC_QPREP(8);
+    else return hipErrorInvalidValue;
+#undef IMGREC_QPREP
     return hipGetLastError();
 }
 

@@ -7,8 +7,8 @@ export PYTHONPATH=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 TAG=${1:-r01}; OUT=gpurun_out/traffic_$TAG; mkdir -p $OUT
 B="python3 bench.py --profile-only --steps 3 --warmup 1 ${BENCH_ARGS:-}"
-timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex knn_tile --pmc FETCH_SIZE -d $OUT/f -o run --output-format csv -- $B > $OUT/f.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex knn_tile --pmc WRITE_SIZE -d $OUT/w -o run --output-format csv -- $B > $OUT/w.log 2>&1 || exit 2
+timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex 'knn_tile|knn_b16' --pmc FETCH_SIZE -d $OUT/f -o run --output-format csv -- $B > $OUT/f.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --kernel-include-regex 'knn_tile|knn_b16' --pmc WRITE_SIZE -d $OUT/w -o run --output-format csv -- $B > $OUT/w.log 2>&1 || exit 2
 python3 - "$OUT" "$TAG" <<'PY'
 import csv, json, sys, collections
 out, tag = sys.argv[1], sys.argv[2]
