@@ -35,8 +35,17 @@
 
 #include "knn_kernels.h"
 
-#ifndef IMGREC_B16_DMA_SPREAD      // 1: DMA halves between k-steps 0/1 (measured slower: 4.48
-#define IMGREC_B16_DMA_SPREAD 0    //    vs 4.25 ms); 0: both halves at the stage start
+// Stage depth (32-bit words per staged row: 32 = 64 bf16, 16 = 32 bf16) and LDS ring depth.
+// 32 x 2: one barrier per 64-deep stage, the next stage's DMA in flight during one stage;
+// 16 x 4: a barrier per 32-deep stage, DMA issued three stages ahead.
+#ifndef IMGREC_B16_BKW
+#define IMGREC_B16_BKW 32
+#endif
+#ifndef IMGREC_B16_RING
+#define IMGREC_B16_RING 2
+#endif
+#ifndef IMGREC_B16_QB_PER_XCD      // query blocks per XCD group (see the block map)
+#define IMGREC_B16_QB_PER_XCD 4
 #endif
 
 namespace imgrec {
@@ -49,18 +58,25 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kNW = 8;                    // waves: 2 along rows x 4 along queries
 constexpr int kBM = kB16BigRows;          // 256 corpus rows per tile
 constexpr int kBQ = kB16BigQueries;       // 256 queries per workgroup
-constexpr int kBKW = 32;                  // 32-bit words (2 bf16) per staged row
-constexpr int kRowB = kBKW * 4;           // 128 B
+constexpr int kBKW = IMGREC_B16_BKW;      // 32-bit words (2 bf16) per staged row: 16 or 32
+constexpr int kNS = IMGREC_B16_RING;      // stages in the LDS ring
+constexpr int kRowB = kBKW * 4;           // bytes per staged row
+constexpr int kCPR = kBKW / 4;            // 16-B chunks per staged row
+constexpr int kKS = kCPR / 2;             // 16-deep MFMA k-steps per stage (chunks per lane half)
+constexpr int kRPP = 64 / kCPR;           // rows per one-KiB DMA piece
+constexpr int kRPB = 64 / kBKW;           // rows per 256-B bank row
 constexpr int kSA = kBM * kRowB;          // A (corpus) stage bytes
 constexpr int kSB = kBQ * kRowB;          // B (query) stage bytes
-constexpr int kStage = kSA + kSB;         // 64 KiB
-constexpr int kNS = 2;
-constexpr int kLPW = (kBM + kBQ) / 8 / kNW;   // one-KiB pieces (8 rows x 128 B) per wave per stage
+constexpr int kStage = kSA + kSB;
+constexpr int kLPW = (kBM + kBQ) / kRPP / kNW;   // pieces per wave per stage (8 or 4)
+constexpr int kNormSlots = 4;             // row-norm ring (tiles)
 constexpr int kNormOff = kNS * kStage;
-constexpr int kLDS = kNormOff + kNS * kBM * 4;
+constexpr int kLDS = kNormOff + kNormSlots * kBM * 4;
+static_assert(kBKW == 16 || kBKW == 32, "stage depth");
 static_assert(kLDS <= 160 * 1024, "LDS budget");
-static_assert(kLPW == 8, "two dma4x halves of four pieces");
+static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
 static_assert(kNW * 16 * 64 * 4 <= kStage, "epilogue parking must fit in one stage");
+static_assert(kNS >= 2 && kNS <= 4, "ring depth");
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
     return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
@@ -69,7 +85,8 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // Four one-KiB LDS-DMA pieces under ONE M0 value: the instruction offset (j KiB) moves both the
 // global source and the LDS destination (measured, tools/micro/glds_offset.hip), so the per-lane
 // offsets v[j] are pre-reduced by j KiB.
-__device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, const uint32_t (&v)[8], int h) {
+template <int N>
+__device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, const uint32_t (&v)[N], int h) {
     unsigned keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
@@ -149,8 +166,13 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int nwg = gridDim.x, wg = blockIdx.x;
     const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
-    const int qb = wgid % nqb;
-    const int split = wgid / nqb;
+    // G query blocks per row split group on one XCD (G = nqb: all query blocks of a split share
+    // its corpus tiles through that XCD's L2; smaller G keeps fewer query blocks per L2)
+    constexpr int kG = IMGREC_B16_QB_PER_XCD;
+    const int G = (nqb % kG == 0) ? kG : nqb;
+    const int qbg = wgid / (nsplit * G), rem = wgid - qbg * (nsplit * G);
+    const int split = rem / G;
+    const int qb = qbg * G + rem % G;
     const int t0 = (int)((int64_t)split * ntiles / nsplit);
     const int t1 = (int)((int64_t)(split + 1) * ntiles / nsplit);
 
@@ -165,27 +187,27 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     if (L2) { qn[0] = qnorm[qcol[0]]; qn[1] = qnorm[qcol[1]]; }
     asm volatile("" : "+v"(qn[0]), "+v"(qn[1]));   // consume the loads before the DMA stream
 
-    // DMA pieces of this wave: 8 consecutive pieces of the A tile (waves 0-3) or B tile (4-7);
+    // DMA pieces of this wave: kLPW consecutive pieces of the A tile (waves 0-3) or B tile (4-7);
     // lane -> (row prow of the piece, chunk pchk), source chunk pre-swizzled.
     const bool isA = wave < 4;
     const int pbase = (isA ? wave : wave - 4) * kLPW;          // first piece index in its tile
-    const int prow = lane >> 3, pchk = lane & 7;
+    const int prow = lane / kCPR, pchk = lane % kCPR;
     uint32_t voff[kLPW];
 #pragma unroll
     for (int j = 0; j < kLPW; ++j) {
-        const int r = (pbase + j) * 8 + prow;
-        // minus the instruction offset dma4x adds to piece j (>= 0: row r >= 8j, dw >= 32)
-        voff[j] = (uint32_t)((r * dw + 4 * (pchk ^ ((r >> 1) & 7))) * 4 - 1024 * (j & 3));
+        const int r = (pbase + j) * kRPP + prow;
+        // minus the instruction offset dma4x adds to piece j (>= 0: row r >= kRPP j, dw >= 32)
+        voff[j] = (uint32_t)((r * dw + 4 * (pchk ^ ((r / kRPB) % kCPR))) * 4 - 1024 * (j & 3));
     }
     const uint32_t smem0 = lds_u32(smem);
     const uint32_t pdst = (uint32_t)((isA ? 0 : kSA) + pbase * 1024);
 
     // fragment read offsets (bytes, inside a stage): k-step c of this lane half = logical chunk
-    // lh*4 + c of row li of each 32-row block
-    const int fsw = (li >> 1) & 7;
-    int aoff[4];
+    // lh*kKS + c of row li of each 32-row block (the swizzle of row li is the same in every block)
+    const int fsw = (li / kRPB) % kCPR;
+    int aoff[kKS];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) aoff[c] = (wr * 128 + li) * kRowB + 16 * ((lh * 4 + c) ^ fsw);
+    for (int c = 0; c < kKS; ++c) aoff[c] = (wr * 128 + li) * kRowB + 16 * ((lh * kKS + c) ^ fsw);
     const int boff = kSA + (wq * 64 - wr * 128) * kRowB;       // B fragment = A offset + boff
 
     float kd[2][KM];
@@ -199,21 +221,29 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int total = (t1 - t0) * nst;
     const uint32_t* qblk = qh + (size_t)qb * kBQ * dw;
 
-    // DMA of stage g, half h (pieces 4h..4h+3; half 0 also the tile's row norms)
-    auto issue_half = [&](int g, int h) __attribute__((always_inline)) {
+    // DMA of stage g into ring slot g % kNS (+ the tile's row norms with its first stage)
+    auto issue = [&](int g) __attribute__((always_inline)) {
         const int it = t0 + g / nst, is = g - (g / nst) * nst;
-        const int buf = g & 1;
         const uint32_t* src = (isA ? xh + (size_t)it * kBM * dw : qblk) + is * kBKW;
-        dma4x(src, smem0 + (uint32_t)(buf * kStage) + pdst + 4096u * h, voff, h);
-        if (h == 0 && is == 0 && wave < 4)                      // the tile's 256 row norms
+        const uint32_t dst = smem0 + (uint32_t)((g % kNS) * kStage) + pdst;
+#pragma unroll
+        for (int h = 0; h < kLPW / 4; ++h) dma4x(src, dst + 4096u * h, voff, h);
+        if (is == 0 && wave < 4)
             dma4_norm(xnorm + (size_t)it * kBM + wave * 64 + lane,
-                      smem0 + (uint32_t)(kNormOff + ((it - t0) & 1) * kBM * 4 + wave * 256));
+                      smem0 + (uint32_t)(kNormOff + ((it - t0) % kNormSlots) * kBM * 4 + wave * 256));
+    };
+    // wait until this wave's DMA of stage g has landed, given stages <= gi were issued
+    auto wait_stage = [&](int g, int gi) __attribute__((always_inline)) {
+        const int newer = gi - g;                               // stages issued after g
+        if (newer >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * kLPW) : "memory");
+        else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kLPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
 
+    int gi = -1;                                                // last stage issued
+    for (int p = 0; p < kNS - 1 && p < total; ++p) issue(++gi);
     if (total > 0) {
-        issue_half(0, 0);
-        issue_half(0, 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wait_stage(0, gi);
         barrier_lds();
     }
 
@@ -228,16 +258,13 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 
         int buf = 0;
         for (int s = 0; s < nst; ++s, ++g) {
-            buf = g & 1;
-            // the next stage's DMA goes into the buffer read last stage, in two halves placed
-            // between k-steps (issue cost hides behind the MFMAs already queued)
+            buf = g % kNS;
+            // stage g + kNS - 1 goes into the slot read during stage g - 1 (every wave passed the
+            // barrier that ended it)
 #ifdef IMGREC_ABLATE_NO_DMA
-            const bool dma_next = g + 1 < total && s == 0;      // ablation: norms + one stage per tile
+            if (gi + 1 < total && s == 0) issue(++gi);          // ablation: norms + a stage per tile
 #else
-            const bool dma_next = g + 1 < total;
-#endif
-#if !IMGREC_B16_DMA_SPREAD
-            if (dma_next) { issue_half(g + 1, 0); issue_half(g + 1, 1); }
+            if (gi + 1 < total) issue(++gi);
 #endif
             const char* sb = smem + buf * kStage;
             u32x4 fa[2][4], fb[2][2];
@@ -248,9 +275,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             for (int h = 0; h < 2; ++h)
                 fb[0][h] = *reinterpret_cast<const u32x4*>(sb + aoff[0] + boff + h * 32 * kRowB);
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < kKS; ++c) {
                 const int cur = c & 1, nxt = cur ^ 1;
-                if (c < 3) {
+                if (c + 1 < kKS) {
 #pragma unroll
                     for (int rb = 0; rb < 4; ++rb)
                         fa[nxt][rb] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + rb * 32 * kRowB);
@@ -258,13 +285,6 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     for (int h = 0; h < 2; ++h)
                         fb[nxt][h] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + boff + h * 32 * kRowB);
                 }
-#if IMGREC_B16_DMA_SPREAD
-                if (c < 2) {                                    // half c between k-steps (A/B knob)
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (dma_next) issue_half(g + 1, c);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#endif
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -277,7 +297,8 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 #ifdef IMGREC_ABLATE_NO_WAIT
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            if (g + 1 < total) wait_stage(g + 1, gi);
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
             if (s + 1 < nst) barrier_lds();
         }
@@ -285,7 +306,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         // ---- epilogue: every wave's fragment reads of the spent stage `buf` are done after this
         // barrier; keys are parked there (the next DMA into `buf` is issued after the next one).
         barrier_lds();
-        const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) & 1) * kBM * 4);
+        const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         float* park = reinterpret_cast<float*>(smem + buf * kStage) + wave * (16 * 64);
         const bool full = row0 + kBM <= nrows;
 #pragma unroll

@@ -230,6 +230,9 @@ struct knn_index {
     uint16_t* qb16 = nullptr; size_t qb16_cap = 0;
     float* q_resid = nullptr; size_t q_resid_cap = 0;
     float* floor = nullptr; size_t floor_cap = 0;
+    float* mws_d = nullptr; size_t mws_d_cap = 0;          // two-level candidate merge workspace
+    int64_t* mws_i = nullptr; size_t mws_i_cap = 0;
+    float* mws_f = nullptr; size_t mws_f_cap = 0;
     size_t xr_max_cap = 0;
     // cascade workspace (queries a candidate pass could not certify, re-run by the next path)
     float* cs_q = nullptr; size_t cs_q_cap = 0;
@@ -380,10 +383,15 @@ int refresh_maxima(knn_index* ix, hipStream_t st) {
     return KNN_OK;
 }
 
+// AUTO: large batches are matrix-bound (bf16 MFMA vs fp32 MFMA) once the corpus amortises the
+// rerank; small batches are HBM-bound (the bf16 copy streams half the bytes) once the corpus is
+// large enough to repay the candidate path's fixed cost (~0.1-0.2 ms).
+constexpr int64_t kB16MinRowsLarge = 16384, kB16MinRowsSmall = 131072;
 bool use_b16(const knn_index* ix, int64_t nq, int k) {
     if (!ix->b16_ok || k > KNN_MAX_K) return false;
     if (ix->mode == KNN_SEARCH_BF16) return true;
-    return ix->mode == KNN_SEARCH_AUTO && nq > 128 && ix->ntotal >= 16384;
+    if (ix->mode != KNN_SEARCH_AUTO) return false;
+    return ix->ntotal >= (nq > 128 ? kB16MinRowsLarge : kB16MinRowsSmall);
 }
 
 bool use_split(const knn_index* ix, int64_t nq, int k) {
@@ -455,9 +463,15 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
     KNN_HIP(p.big ? imgrec::launch_b16_big(a, st) : imgrec::launch_tile_topk(a, st));
     if (e1) KNN_HIP(hipEventRecord(e1, st));
-    KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, p.ncand / km, km, p.ncand,
-                                            km, kc, ix->id_offset, ix->cand2_d, ix->cand2_i,
-                                            ix->floor, st));
+    const int nlists = p.ncand / km, ngrp = (nlists + 63) / 64;
+    if (ngrp > 1) {
+        if ((rc = grow(&ix->mws_d, &ix->mws_d_cap, (size_t)nq * ngrp * 16)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * 16)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
+    }
+    KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
+                                            ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
+                                            ix->mws_d, ix->mws_i, ix->mws_f, st));
     KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
     KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
     imgrec::RerankArgs r{};
@@ -654,7 +668,8 @@ int knn_free(knn_index_t* ix) {
     (void)hipStreamSynchronize(ix->stream);
     for (void* p : {(void*)ix->xh, (void*)ix->xr, (void*)ix->xr_max, (void*)ix->qb16,
                     (void*)ix->q_resid, (void*)ix->floor, (void*)ix->cs_q, (void*)ix->cs_qn,
-                    (void*)ix->cs_d, (void*)ix->cs_i, (void*)ix->cs_list})
+                    (void*)ix->cs_d, (void*)ix->cs_i, (void*)ix->cs_list, (void*)ix->mws_d,
+                    (void*)ix->mws_i, (void*)ix->mws_f})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
                     (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,

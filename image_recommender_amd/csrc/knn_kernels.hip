@@ -735,20 +735,27 @@ __device__ __forceinline__ float key_from_ordered(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
+// A query's nlists lists may be split into G groups of <= 64 (two-level merge): wave s handles
+// group s % G of query s / G; floor_in (optional, G per output row of the previous level) is
+// folded into the output floor.
 template <int KIN>
 __global__ void __launch_bounds__(256)
-cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
-                       int nlists, int64_t stride_q, int64_t stride_l, int kout, int64_t id_offset,
+cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nsub,
+                       int nlists, int G, int64_t stride_q, int64_t stride_l, int kout,
+                       int64_t id_offset, const float* __restrict__ floor_in, int G_in,
                        float* __restrict__ D, int64_t* __restrict__ I, float* __restrict__ floor_out) {
     const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;                                        // whole wave
+    const int64_t sq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sq >= nsub) return;                                     // whole wave
+    const int64_t q = sq / G;
+    const int grp = (int)(sq - q * G);
+    const int nl = min(64, nlists - 64 * grp);                  // lists of this group
     constexpr uint64_t kEmpty = ~0ull;
     uint64_t v[KIN];
-    float fl = INFINITY;
-    if (lane < nlists) {
-        const float* lp = cd + q * stride_q + (int64_t)lane * stride_l;
-        const int64_t* ip = ci + q * stride_q + (int64_t)lane * stride_l;
+    float fl = (floor_in && lane < G_in) ? floor_in[sq * G_in + lane] : INFINITY;
+    if (lane < nl) {
+        const float* lp = cd + q * stride_q + (int64_t)(64 * grp + lane) * stride_l;
+        const int64_t* ip = ci + q * stride_q + (int64_t)(64 * grp + lane) * stride_l;
 #pragma unroll
         for (int p = 0; p < KIN; ++p) {
             const float kv = lp[p];
@@ -763,7 +770,7 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
-    if (lane == 0) floor_out[q] = fl;
+    if (lane == 0) floor_out[sq] = fl;
     for (int r = 0; r < kout; ++r) {
         uint64_t b = v[0];
 #pragma unroll
@@ -779,8 +786,8 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
             v[KIN - 1] = kEmpty;
         }
         if (lane == 0) {
-            D[q * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
-            I[q * kout + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b + id_offset;
+            D[sq * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
+            I[sq * kout + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b + id_offset;
         }
     }
 }
@@ -788,16 +795,32 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,
                                    int64_t id_offset, float* D, int64_t* I, float* floor,
-                                   hipStream_t st) {
+                                   float* ws_d, int64_t* ws_i, float* ws_floor, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
     if (kout <= 0 || kout > 64 || !floor) return hipErrorInvalidValue;
-    if (nlists <= 64 && (kin == 8 || kin == 10 || kin == 16)) {
-        const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
-#define IMGREC_CAND_LANE(KV) hipLaunchKernelGGL((cand_merge_lane_kernel<KV>), grid, block, 0, st, cd, ci, \
-                                                nq, nlists, stride_q, stride_l, kout, id_offset, D, I, floor)
-        if (kin == 8) IMGREC_CAND_LANE(8);
-        else if (kin == 10) IMGREC_CAND_LANE(10);
-        else IMGREC_CAND_LANE(16);
+    const int G = (nlists + 63) / 64;
+    if ((kin == 8 || kin == 10 || kin == 16) && G <= 64 && (G == 1 || (ws_d && ws_i && ws_floor))) {
+#define IMGREC_CAND_LANE(KV, NSUB, NL, GG, SQ, SL, KO, FIN, GIN, OD, OI, OF)                      \
+        hipLaunchKernelGGL((cand_merge_lane_kernel<KV>), dim3((unsigned)(((NSUB) + 3) / 4)), dim3(256), \
+                           0, st, cd_, ci_, NSUB, NL, GG, SQ, SL, KO, id_offset, FIN, GIN, OD, OI, OF)
+        const float* cd_ = cd;
+        const int64_t* ci_ = ci;
+        if (G == 1) {
+            if (kin == 8) IMGREC_CAND_LANE(8, nq, nlists, 1, stride_q, stride_l, kout, nullptr, 0, D, I, floor);
+            else if (kin == 10) IMGREC_CAND_LANE(10, nq, nlists, 1, stride_q, stride_l, kout, nullptr, 0, D, I, floor);
+            else IMGREC_CAND_LANE(16, nq, nlists, 1, stride_q, stride_l, kout, nullptr, 0, D, I, floor);
+            return hipGetLastError();
+        }
+        // level 1: each group of 64 lists -> its 16 best (+ floor); level 2: the G lists of 16
+        const int64_t nsub = nq * (int64_t)G;
+        if (kin == 8) IMGREC_CAND_LANE(8, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+        else if (kin == 10) IMGREC_CAND_LANE(10, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+        else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        cd_ = ws_d;
+        ci_ = ws_i;
+        IMGREC_CAND_LANE(16, nq, G, 1, (int64_t)G * 16, 16, kout, ws_floor, G, D, I, floor);
 #undef IMGREC_CAND_LANE
         return hipGetLastError();
     }

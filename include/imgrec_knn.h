@@ -63,9 +63,10 @@ enum knn_error {
  * computes their exact keys and a per-query error-bound certificate proves that no row outside
  * the candidates can rank before a returned one; uncertified queries re-run on a more precise
  * path (bf16 -> split when more than 128 fail, else -> exact fp32 kernel).
- * AUTO: batches of > 128 queries on an index of >= 16384 rows take the bf16 path (d >= 64; one
- *       bf16 MFMA per product, K' = 64), or the split path when bf16 is unavailable; everything
- *       else the exact fp32 kernel.
+ * AUTO: the bf16 path (d >= 64; one bf16 MFMA per product, K' = 64) for batches of > 128
+ *       queries on an index of >= 16384 rows and for smaller batches on an index of >= 131072
+ *       rows (the bf16 copy streams half the bytes); the split path when bf16 is unavailable and
+ *       the batch is large; everything else the exact fp32 kernel.
  * EXACT: always the fp32 kernel.  SPLIT: the split path (bf16 hi/lo, three MFMAs per product,
  *       K' = 16/32) whenever k <= 16 and d >= 256.  BF16: the bf16 path for every batch (tests).
  * A candidate-path search synchronises its stream once per 8192-query chunk (certificate count). */

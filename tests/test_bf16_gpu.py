@@ -239,3 +239,21 @@ def test_bf16_big_tile_self_query_concat(faiss):
     assert ncand == 1024 and nfb <= 100
     assert (I[:, 0] == np.arange(1024)).all()
     np.testing.assert_allclose(D[:, 0], 4 - 2 * np.sqrt(3), rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("nq", [1, 5, 64])
+def test_auto_small_batch_on_large_corpus_takes_bf16(faiss, nq):
+    """AUTO routes small batches on corpora of >= 131072 rows to the bf16 path (HBM-bound: the
+    bf16 copy streams half the bytes); many row splits per query exercise the two-level
+    candidate merge."""
+    xb = mixture(140000, 256, centres=300, seed=41)
+    xq = mixture(nq, 256, centres=300, seed=42)
+    idx = faiss.IndexFlatL2(256)
+    idx.add(xb)
+    D, I = idx.search(xq, 10)
+    assert idx.search_stats()[0] == nq
+    _bound_holds(idx)
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+    for k in (1, 16, 32):
+        D, I = idx.search(xq, k)
+        check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)
