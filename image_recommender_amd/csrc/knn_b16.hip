@@ -25,6 +25,14 @@
 // per 256-B bank row); the XOR is applied on the DMA's per-lane global source offset, so every
 // ds_read_b128 lane group of 16 hits 16 distinct bank slots.
 //
+// Row splits: the corpus is cut into groups of kRPP rows (one DMA piece each); split s owns the
+// global groups s, s + nsplit, s + 2 nsplit, ... and a tile holds kGPT consecutive groups of its
+// split.  A stored order that keeps similar rows together (the reference stores images folder by
+// folder) is thereby spread over every split, so no split's short list has to hold most of a
+// query's neighbours — with contiguous splits the merge floor bound on such corpora and sent a
+// quarter of the queries to the exact re-run.  A tile's pieces sit nsplit * kRPP rows apart: the
+// per-lane offsets stay fixed, the scalar base moves by kGPT groups per tile.
+//
 // Accumulator map (v_mfma_f32_32x32x16_bf16): col = lane & 31 -> query, row = (reg & 3) +
 // 8 (reg >> 2) + 4 (lane >> 5) -> corpus row: each lane owns two queries (one per query block)
 // and 16 rows of each row block, so the top-k needs no data movement.
@@ -65,6 +73,7 @@ constexpr int kCPR = kBKW / 4;            // 16-B chunks per staged row
 constexpr int kKS = kCPR / 2;             // 16-deep MFMA k-steps per stage (chunks per lane half)
 constexpr int kRPP = 64 / kCPR;           // rows per one-KiB DMA piece
 constexpr int kRPB = 64 / kBKW;           // rows per 256-B bank row
+constexpr int kGPT = kBM / kRPP;          // row groups (= A pieces) per tile
 constexpr int kSA = kBM * kRowB;          // A (corpus) stage bytes
 constexpr int kSB = kBQ * kRowB;          // B (query) stage bytes
 constexpr int kStage = kSA + kSB;
@@ -157,7 +166,7 @@ template <int KM, int L2>
 __global__ void __launch_bounds__(512, 2)
 knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ xnorm, int nrows,
                     int dw, const uint32_t* __restrict__ qh, const float* __restrict__ qnorm, int nq,
-                    int ntiles, int nsplit, int nqb, int64_t id_offset, float* __restrict__ cand_d,
+                    int nsplit, int nqb, int64_t id_offset, float* __restrict__ cand_d,
                     int64_t* __restrict__ cand_i, int ncand) {
     __shared__ __attribute__((aligned(16))) char smem[kLDS];
 
@@ -173,8 +182,16 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int qbg = wgid / (nsplit * G), rem = wgid - qbg * (nsplit * G);
     const int split = rem / G;
     const int qb = qbg * G + rem % G;
-    const int t0 = (int)((int64_t)split * ntiles / nsplit);
-    const int t1 = (int)((int64_t)(split + 1) * ntiles / nsplit);
+    // this split's rows (header): cnt groups, global group split + m * nsplit for m < cnt, tile t
+    // = groups t * kGPT .. + kGPT - 1 of the split (the last tile may hold fewer)
+    const int ngroups = (nrows + kRPP - 1) / kRPP;
+    const int cnt = split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0;
+    const int t0 = 0, t1 = (cnt + kGPT - 1) / kGPT;
+    // stored row of tile row tr of tile t (groups past the split's end: the tile's first group)
+    auto trow = [&](int t, int tr) {
+        const int m = t * kGPT + tr / kRPP;
+        return (split + (m < cnt ? m : t * kGPT) * nsplit) * kRPP + tr % kRPP;
+    };
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -192,13 +209,21 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const bool isA = wave < 4;
     const int pbase = (isA ? wave : wave - 4) * kLPW;          // first piece index in its tile
     const int prow = lane / kCPR, pchk = lane % kCPR;
+    // Per-piece lane offsets in bytes from the stage's scalar base, minus the instruction offset
+    // dma4x adds to piece j.  The base sits 4 KiB below the tile's first row (corpus) or the
+    // query block, so an offset stays >= 0 when a piece past the split's end is clamped to the
+    // tile's first group (ng = groups the tile holds).
     uint32_t voff[kLPW];
+    auto set_voff = [&](int ng) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < kLPW; ++j) {
-        const int r = (pbase + j) * kRPP + prow;
-        // minus the instruction offset dma4x adds to piece j (>= 0: row r >= kRPP j, dw >= 32)
-        voff[j] = (uint32_t)((r * dw + 4 * (pchk ^ ((r / kRPB) % kCPR))) * 4 - 1024 * (j & 3));
-    }
+        for (int j = 0; j < kLPW; ++j) {
+            const int P = pbase + j, r = P * kRPP + prow;          // r: LDS row of this lane
+            const int srow = isA ? (P < ng ? P * nsplit * kRPP : 0) + prow : r;
+            voff[j] = (uint32_t)srow * (uint32_t)(dw * 4) +
+                      16u * (uint32_t)(pchk ^ ((r / kRPB) % kCPR)) + 4096u - 1024u * (uint32_t)(j & 3);
+        }
+    };
+    set_voff(kGPT);
     const uint32_t smem0 = lds_u32(smem);
     const uint32_t pdst = (uint32_t)((isA ? 0 : kSA) + pbase * 1024);
 
@@ -224,12 +249,14 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     // DMA of stage g into ring slot g % kNS (+ the tile's row norms with its first stage)
     auto issue = [&](int g) __attribute__((always_inline)) {
         const int it = t0 + g / nst, is = g - (g / nst) * nst;
-        const uint32_t* src = (isA ? xh + (size_t)it * kBM * dw : qblk) + is * kBKW;
+        if (isA && is == 0 && it == t1 - 1 && cnt - it * kGPT < kGPT) set_voff(cnt - it * kGPT);
+        const uint32_t* src = (isA ? xh + (size_t)trow(it, 0) * dw : qblk) + is * kBKW;
+        const char* sbase = reinterpret_cast<const char*>(src) - 4096;
         const uint32_t dst = smem0 + (uint32_t)((g % kNS) * kStage) + pdst;
 #pragma unroll
-        for (int h = 0; h < kLPW / 4; ++h) dma4x(src, dst + 4096u * h, voff, h);
+        for (int h = 0; h < kLPW / 4; ++h) dma4x(sbase, dst + 4096u * h, voff, h);
         if (is == 0 && wave < 4)
-            dma4_norm(xnorm + (size_t)it * kBM + wave * 64 + lane,
+            dma4_norm(xnorm + trow(it, wave * 64 + lane),
                       smem0 + (uint32_t)(kNormOff + ((it - t0) % kNormSlots) * kBM * 4 + wave * 256));
     };
     // wait until this wave's DMA of stage g has landed, given stages <= gi were issued
@@ -249,7 +276,6 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 
     int g = 0;
     for (int t = t0; t < t1; ++t) {
-        const int row0 = t * kBM;
         f32x16 acc[4][2];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
@@ -308,11 +334,14 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         barrier_lds();
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         float* park = reinterpret_cast<float*>(smem + buf * kStage) + wave * (16 * 64);
-        const bool full = row0 + kBM <= nrows;
+        // every group of the tile belongs to the split and the last one holds kRPP stored rows
+        const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
+        // tile row tr counts iff its group belongs to the split and its stored row is < nrows
+        auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
 #ifdef IMGREC_ABLATE_NO_EPILOGUE
-            if (qcol[h] >= nq || row0 >= 0) continue;          // ablation: keeps acc live only
+            if (qcol[h] >= nq || t >= 0) continue;             // ablation: keeps acc live only
 #else
             if (qcol[h] >= nq) continue;
 #endif
@@ -339,7 +368,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                             kv = -acc[rb][h][r];
                         }
                         key[r] = kv;
-                        const bool pass = (full || row0 + rbase + 8 * j + i < nrows) && kv < tau &&
+                        const bool pass = (full || row_ok(rbase + 8 * j + i)) && kv < tau &&
                                           kv <= tau_p;
                         mask |= (unsigned)pass << r;
                     }
@@ -353,7 +382,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                             const int r = __builtin_ctz(m);
                             m &= m - 1u;
                             const float kv = park[r * 64 + lane];
-                            const int row = row0 + rbase + (r & 3) + 8 * (r >> 2);
+                            const int row = trow(t, rbase + (r & 3) + 8 * (r >> 2));
                             if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, row);
                         }
                     }
@@ -409,13 +438,16 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 }
 
 hipError_t launch_b16_big(const TileArgs& a, hipStream_t st) {
-    if (a.wr != 2 || a.wq != 4 || a.dp % kBKW != 0) return hipErrorInvalidValue;
+    if (a.wr != 2 || a.wq != 4 || a.dp % kBKW != 0 || a.nsplit < 1) return hipErrorInvalidValue;
+    // the lane offsets are 32-bit: a tile's last group sits (kGPT - 1) * nsplit groups past its first
+    if (((int64_t)(kGPT - 1) * a.nsplit * kRPP + kBQ) * a.dp * 4 + 8192 >= ((int64_t)1 << 32))
+        return hipErrorInvalidValue;
     const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(kNW * 64);
     const uint32_t* xh = reinterpret_cast<const uint32_t*>(a.xb);
     const uint32_t* qh = reinterpret_cast<const uint32_t*>(a.qp);
 #define IMGREC_LAUNCH_B16(KMV, L2V)                                                                \
     hipLaunchKernelGGL((knn_b16_tile_kernel<KMV, L2V>), grid, block, 0, st, xh, a.xnorm, a.nrows,  \
-                       a.dp, qh, a.qnorm, a.nq, a.ntiles, a.nsplit, a.nqb, a.id_offset, a.cand_d,   \
+                       a.dp, qh, a.qnorm, a.nq, a.nsplit, a.nqb, a.id_offset, a.cand_d,             \
                        a.cand_i, a.ncand)
     if (a.km == 8) {
         if (a.metric == 1) IMGREC_LAUNCH_B16(8, 1); else IMGREC_LAUNCH_B16(8, 0);

@@ -163,9 +163,10 @@ inline int b16_km(int k) { return k <= 16 ? 16 : 32; }
 
 // bf16-path geometry: large batches with k <= 10 on the 256 x 256-tile kernel (one workgroup
 // per CU, lane lists of 8 / 10); otherwise (kB16WR, kB16WQ) workgroups, kB16WGPCU per CU.
-Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus) {
+Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus, int dpb) {
     Plan p{};
-    if (nq >= imgrec::kB16BigMinQ && k <= 10) {
+    // (dpb bound: the 256 x 256 kernel's 32-bit lane offsets, see launch_b16_big)
+    if (nq >= imgrec::kB16BigMinQ && k <= 10 && dpb <= 16384) {
         p.big = true;
         p.km = k <= 8 ? 8 : 10;
         p.wr = 2;
@@ -438,7 +439,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
               int64_t* I, hipStream_t st, bool timed, bool q_ready) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = kB16Cand;
-    const Plan p = make_b16_plan(ix->ntotal, nq, k, ix->cus);
+    const Plan p = make_b16_plan(ix->ntotal, nq, k, ix->cus, ix->dpb);
     const int km = p.km;
     int rc;
     if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
@@ -465,8 +466,8 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     if (e1) KNN_HIP(hipEventRecord(e1, st));
     const int nlists = p.ncand / km, ngrp = (nlists + 63) / 64;
     if (ngrp > 1) {
-        if ((rc = grow(&ix->mws_d, &ix->mws_d_cap, (size_t)nq * ngrp * 16)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * 16)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_d, &ix->mws_d_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
         if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
     }
     KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
@@ -575,7 +576,7 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         const bool b16 = use_b16(ix, cn, k);
         const bool split = !b16 && use_split(ix, cn, k);
         // padding: the query tile of the plan this chunk will run
-        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus)
+        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                      : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                              : make_plan(ix->ntotal, cn, k, ix->cus);
         const int64_t nq_pad = p.nq_pad;
@@ -877,7 +878,7 @@ int knn_last_path(const knn_index_t* ix) { return ix ? ix->last_path : KNN_EINVA
 int knn_plan(const knn_index_t* ix, int64_t nq, int k, int* tr, int* tq, int* splits, int* wgs) {
     if (!ix || !tr || !tq || !splits || !wgs) KNN_FAIL(KNN_EINVAL, "NULL argument");
     const int64_t cn = std::min(nq, kQueryChunk);
-    const Plan p = use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, k, ix->cus)
+    const Plan p = use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                  : use_split(ix, cn, k) ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                                         : make_plan(ix->ntotal, cn, k, ix->cus);
     *tr = p.bm;

@@ -113,7 +113,7 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
 // Candidate merge for the rerank: nq x kout approximate candidates (ascending raw keys, empty =
 // label -1) and, per query, the floor: the smallest key a row dropped by any list or by the merge's
 // own lane lists can have (+inf when nothing was dropped).
-// ws_*: two-level workspace for more than 64 lists per query (nq * ceil(nlists/64) * 16 entries,
+// ws_*: two-level workspace for more than 64 lists per query (nq * ceil(nlists/64) * kout entries,
 // nq * ceil(nlists/64) floors), may be NULL when nlists <= 64.
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,

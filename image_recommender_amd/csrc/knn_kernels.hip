@@ -240,8 +240,13 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
     const int qb = wgid % nqb;
     const int split = wgid / nqb;
-    const int t0 = (int)((int64_t)split * ntiles / nsplit);
-    const int t1 = (int)((int64_t)(split + 1) * ntiles / nsplit);
+    // this split's tiles, in increasing order: tile(j) for j in [0, t1).  Round-robin (split s
+    // takes tiles s, s + nsplit, ...) spreads rows that are adjacent in storage — the reference
+    // numbers images folder by folder — over many lists, so one list seldom holds a query's
+    // whole neighbourhood (which would pull the certificate's floor down).
+    const int t0 = 0;
+    const int t1 = split < ntiles ? (ntiles - split + nsplit - 1) / nsplit : 0;
+    auto tile = [&](int j) { return split + j * nsplit; };
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -291,13 +296,13 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     const uint32_t smem_u32 = lds_addr(smem);
     const uint32_t norm_u32 = lds_addr(norm_base);
     int it = t0, is = 0, ibuf = 0;
-    const float* itile = xb + (size_t)t0 * BM * dp;     // corpus rows of tile `it`
+    const float* itile = xb + (size_t)tile(t0) * BM * dp;   // corpus rows of tile `it`
     auto issue_next = [&]() __attribute__((always_inline)) {
         if (it >= t1) return;
         const uint32_t st = smem_u32 + (uint32_t)(ibuf * STAGE) * 4u;
         if (is == 0) {                      // row norms of the tile, one 4-B DMA per lane
             for (int j = wave; j < BM / 64; j += NW)
-                dma4(xnorm + (size_t)it * BM + j * 64 + lane,
+                dma4(xnorm + (size_t)tile(it) * BM + j * 64 + lane,
                      norm_u32 + (uint32_t)(((it - t0) % NS) * BM + j * 64) * 4u);
         }
         const int k0 = is * BK;
@@ -308,7 +313,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #endif
             dma16((pis_a[j] ? itile : qbase) + poff[j] + k0, st + pdst[j]);
         }
-        if (++is == nsteps) { is = 0; ++it; itile += (size_t)BM * dp; }
+        if (++is == nsteps) { is = 0; ++it; itile += (size_t)nsplit * BM * dp; }
         ibuf = (ibuf + 1 == NS) ? 0 : ibuf + 1;
     };
 
@@ -322,7 +327,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     PROF_T(tk0);
 #endif
     for (int t = t0; t < t1; ++t) {
-        const int row0 = t * BM;
+        const int row0 = tile(t) * BM;
         f32x16 acc[WB];
 #pragma unroll
         for (int b = 0; b < WB; ++b) acc[b] = (f32x16){0.f};
@@ -792,6 +797,53 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
     }
 }
 
+// Second level of the two-level merge: up to 64 packed lists of up to 64 entries per query, the
+// lane queues in LDS with a head index each (one wave per query).  Inputs are the first level's
+// outputs: (key, global label) sorted ascending, plus G floors per query.
+__global__ void __launch_bounds__(64)
+cand_merge_lds_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
+                      int nlists, int kin, int kout, int64_t id_offset,
+                      const float* __restrict__ floor_in, float* __restrict__ D,
+                      int64_t* __restrict__ I, float* __restrict__ floor_out) {
+    __shared__ uint64_t qv[64 * 65];                  // lane l's queue at qv[l * 65 ...]
+    const int lane = threadIdx.x;
+    const int64_t q = blockIdx.x;
+    constexpr uint64_t kEmpty = ~0ull;
+    float fl = lane < nlists ? floor_in[q * nlists + lane] : INFINITY;
+    if (lane < nlists) {
+        const float* lp = cd + (q * nlists + lane) * kin;
+        const int64_t* ip = ci + (q * nlists + lane) * kin;
+        for (int p = 0; p < kin; ++p) {
+            const int64_t lab = ip[p];
+            qv[lane * 65 + p] = lab < 0 ? kEmpty
+                                        : ((uint64_t)key_bits_ordered(lp[p]) << 32) | (uint32_t)(lab - id_offset);
+        }
+        if (ip[kin - 1] >= 0) fl = fminf(fl, lp[kin - 1]);
+    }
+    for (int p = (lane < nlists ? kin : 0); p <= 64; ++p) qv[lane * 65 + p] = kEmpty;
+    __syncthreads();
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+    if (lane == 0) floor_out[q] = fl;
+    int head = 0;
+    uint64_t cur = qv[lane * 65];
+    for (int r = 0; r < kout; ++r) {
+        uint64_t b = cur;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)b, off, 64);
+            const uint32_t hi = __shfl_xor((uint32_t)(b >> 32), off, 64);
+            const uint64_t o = ((uint64_t)hi << 32) | lo;
+            b = o < b ? o : b;
+        }
+        if (b != kEmpty && cur == b) cur = qv[lane * 65 + (++head)];
+        if (lane == 0) {
+            D[q * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
+            I[q * kout + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b + id_offset;
+        }
+    }
+}
+
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,
                                    int64_t id_offset, float* D, int64_t* I, float* floor,
@@ -811,17 +863,17 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
             else IMGREC_CAND_LANE(16, nq, nlists, 1, stride_q, stride_l, kout, nullptr, 0, D, I, floor);
             return hipGetLastError();
         }
-        // level 1: each group of 64 lists -> its 16 best (+ floor); level 2: the G lists of 16
+        // level 1: each group of 64 lists -> its kout best (+ floor: a group that keeps fewer
+        // than kout would cap the certificate at that group's last key); level 2: the G lists
         const int64_t nsub = nq * (int64_t)G;
-        if (kin == 8) IMGREC_CAND_LANE(8, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
-        else if (kin == 10) IMGREC_CAND_LANE(10, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
-        else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+        if (kin == 8) IMGREC_CAND_LANE(8, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
+        else if (kin == 10) IMGREC_CAND_LANE(10, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
+        else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
+#undef IMGREC_CAND_LANE
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        cd_ = ws_d;
-        ci_ = ws_i;
-        IMGREC_CAND_LANE(16, nq, G, 1, (int64_t)G * 16, 16, kout, ws_floor, G, D, I, floor);
-#undef IMGREC_CAND_LANE
+        hipLaunchKernelGGL(cand_merge_lds_kernel, dim3((unsigned)nq), dim3(64), 0, st, ws_d, ws_i, nq,
+                           G, kout, kout, id_offset, ws_floor, D, I, floor);
         return hipGetLastError();
     }
     // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is

@@ -257,3 +257,27 @@ def test_auto_small_batch_on_large_corpus_takes_bf16(faiss, nq):
     for k in (1, 16, 32):
         D, I = idx.search(xq, k)
         check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("nq", [300, 1024])
+def test_bf16_cluster_sorted_storage(faiss, nq):
+    """Rows stored cluster by cluster (the reference numbers images folder by folder, so similar
+    images sit on adjacent rows): results stay exact, and interleaved row splits keep most
+    queries certified (a query's neighbourhood spreads over several per-split lists)."""
+    rng = np.random.default_rng(51)
+    n, d, ncent = 60000, 384, 60
+    cent = rng.standard_normal((ncent, d))
+    lab = np.repeat(np.arange(ncent), n // ncent)                      # contiguous clusters
+    xb = (cent[lab] + 0.5 * rng.standard_normal((n, d))).astype(np.float32)
+    xq = (cent[rng.integers(0, ncent, nq)] + 0.5 * rng.standard_normal((nq, d))).astype(np.float32)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    ncand, nfb = idx.search_stats()
+    assert ncand == nq
+    _bound_holds(idx)
+    sel = np.arange(0, nq, 5)
+    check_knn(D[sel], I[sel], xb, xq[sel], 10, "l2", min_exact_frac=0.5)
+    print(f"cluster-sorted storage: {nfb} of {nq} queries re-run")
+    assert nfb <= nq // 4
