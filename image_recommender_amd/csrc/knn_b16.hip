@@ -19,7 +19,8 @@
 // k-steps (fragments of step c+1 read while step c's 8 MFMAs run), wait for the own DMA, barrier.
 // Measured bound: the per-CU global->LDS rate (~25 B/clk; 64 KiB per stage against 2048 MFMA
 // cycles per SIMD) — spreading the DMA issue between k-steps did not help.  After a tile's last stage: barrier,
-// top-k epilogue (keys parked in the just-consumed stage), barrier.
+// top-k epilogue (accumulators of rows that pass the screen parked in the just-consumed stage),
+// barrier.
 //
 // LDS image: row r of a stage, 16-B chunk c stored at chunk c ^ ((r >> 1) & 7) (two 128-B rows
 // per 256-B bank row); the XOR is applied on the DMA's per-lane global source offset, so every
@@ -62,6 +63,7 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kNW = 8;                    // waves: 2 along rows x 4 along queries
 constexpr int kBM = kB16BigRows;          // 256 corpus rows per tile
@@ -80,7 +82,8 @@ constexpr int kStage = kSA + kSB;
 constexpr int kLPW = (kBM + kBQ) / kRPP / kNW;   // pieces per wave per stage (8 or 4)
 constexpr int kNormSlots = 4;             // row-norm ring (tiles)
 constexpr int kNormOff = kNS * kStage;
-constexpr int kLDS = kNormOff + kNormSlots * kBM * 4;
+constexpr int kShareOff = kNormOff + kNormSlots * kBM * 4;   // per (wave, query): screen bound
+constexpr int kLDS = kShareOff + kNW * 2 * 32 * 4;
 static_assert(kBKW == 16 || kBKW == 32, "stage depth");
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
@@ -241,6 +244,11 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int p = 0; p < KM; ++p) { kd[h][p] = INFINITY; ki[h][p] = -1; }
+    if (lh == 0) {                                              // screen bounds: none yet
+        float* share = reinterpret_cast<float*>(smem + kShareOff);
+        share[((wr * 4 + wq) * 2) * 32 + li] = INFINITY;
+        share[((wr * 4 + wq) * 2 + 1) * 32 + li] = INFINITY;
+    }
 
     const int nst = dw / kBKW;                                  // stages per tile
     const int total = (t1 - t0) * nst;
@@ -311,6 +319,14 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     for (int h = 0; h < 2; ++h)
                         fb[nxt][h] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + boff + h * 32 * kRowB);
                 }
+#ifdef IMGREC_ABLATE_NO_MFMA
+                // ablation: fragments read and consumed, no matrix work
+#pragma unroll
+                for (int rb = 0; rb < 4; ++rb) asm volatile("" ::"v"(fa[cur][rb]));
+#pragma unroll
+                for (int h = 0; h < 2; ++h) asm volatile("" ::"v"(fb[cur][h]));
+                if (nq < 0)
+#endif
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -329,65 +345,100 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             if (s + 1 < nst) barrier_lds();
         }
 
-        // ---- epilogue: every wave's fragment reads of the spent stage `buf` are done after this
-        // barrier; keys are parked there (the next DMA into `buf` is issued after the next one).
-        barrier_lds();
+        // ---- epilogue.  Screen: a row can only matter if its key beats T = min(own K-th, the
+        // partner lane's K-th, max over the query's four lists of their J-th best) — four lists
+        // holding J >= KM/4 entries each at or below that max already give the union KM better
+        // entries; a dropped row ranks behind the folded list's last entry (merge floor).  The
+        // test runs on the accumulator: d = (|x|^2 (1/2 - 2^-20) + c) - acc with c = (|q|^2 -
+        // T)/2 - 2^-20 (|q|^2 + |T|) is negative iff the row passes (the 2^-20 terms keep fp32
+        // rounding from rejecting a row the exact key would keep); two packed adds per pair of
+        // rows and one v_alignbit per row shift the sign bits into a 16-bit lane mask.  Rows a
+        // lane passed: raw accumulators parked in the spent stage, keys computed, inserted.
+        barrier_lds();                                          // spent stage free for parking
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
-        float* park = reinterpret_cast<float*>(smem + buf * kStage) + wave * (16 * 64);
-        // every group of the tile belongs to the split and the last one holds kRPP stored rows
+        float* share = reinterpret_cast<float*>(smem + kShareOff);
+        float4* park = reinterpret_cast<float4*>(smem + buf * kStage) + wave * (4 * 64);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
-        // tile row tr counts iff its group belongs to the split and its stored row is < nrows
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
+        constexpr int kJ = (KM + 3) / 4;
+        constexpr float kLo = 1.0f / 1048576.f;
+        float cth[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-#ifdef IMGREC_ABLATE_NO_EPILOGUE
-            if (qcol[h] >= nq || t >= 0) continue;             // ablation: keeps acc live only
+            const float tau = kd[h][KM - 1];
+            const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
+#ifdef IMGREC_ABLATE_NO_SHARE
+            const float other = INFINITY;
 #else
-            if (qcol[h] >= nq) continue;
+            const float other = share[(((1 - wr) * 4 + wq) * 2 + h) * 32 + li];
 #endif
+            const float T = fminf(fminf(tau, __shfl_xor(tau, 32, 64)), fmaxf(jb, other));
+            float c = L2 ? 0.5f * (qn[h] - T) - kLo * (qn[h] + fabsf(T)) : -T;
+            cth[h] = qcol[h] < nq ? c : INFINITY;
+        }
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb) {
-                const float tau = kd[h][KM - 1];
-                const float tau_p = __shfl_xor(tau, 32, 64);   // partner lane: same query
-                const int rbase = wr * 128 + rb * 32 + 4 * lh;  // tile row of accumulator reg 0
-                float key[16];
-                unsigned mask = 0;
+        for (int rb = 0; rb < 4; ++rb) {
+#ifdef IMGREC_ABLATE_NO_EPILOGUE
+            asm volatile("" ::"v"(acc[rb][0]), "v"(acc[rb][1]));
+            continue;
+#endif
+            const int rbase = wr * 128 + rb * 32 + 4 * lh;      // tile row of accumulator reg 0
+            unsigned live = 0xffffu;                            // rows of the block that count
+            if (!full) {
+                live = 0;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (L2) n4 = *reinterpret_cast<const float4*>(nrm + rbase + 8 * j);
-                    const float nv[4] = {n4.x, n4.y, n4.z, n4.w};
+                for (int r = 0; r < 16; ++r) live |= (unsigned)row_ok(rbase + (r & 3) + 8 * (r >> 2)) << r;
+            }
+            unsigned msk[2] = {0u, 0u};
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = 4 * j + i;
+            for (int j = 3; j >= 0; --j) {                      // rows 4j+3 .. 4j: high bits first
+                float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (L2) n4 = *reinterpret_cast<const float4*>(nrm + rbase + 8 * j);
+                const f32x2 half2 = (f32x2){0.5f - kLo, 0.5f - kLo};
+                const f32x2 hlo = (f32x2){n4.x, n4.y} * half2, hhi = (f32x2){n4.z, n4.w} * half2;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const f32x2 c2 = (f32x2){cth[h], cth[h]};
+                    const f32x2 dhi = (L2 ? hhi + c2 : c2) - (f32x2){acc[rb][h][4 * j + 2], acc[rb][h][4 * j + 3]};
+                    const f32x2 dlo = (L2 ? hlo + c2 : c2) - (f32x2){acc[rb][h][4 * j], acc[rb][h][4 * j + 1]};
+                    msk[h] = __builtin_amdgcn_alignbit(msk[h], __float_as_uint(dhi.y), 31);
+                    msk[h] = __builtin_amdgcn_alignbit(msk[h], __float_as_uint(dhi.x), 31);
+                    msk[h] = __builtin_amdgcn_alignbit(msk[h], __float_as_uint(dlo.y), 31);
+                    msk[h] = __builtin_amdgcn_alignbit(msk[h], __float_as_uint(dlo.x), 31);
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                unsigned m = msk[h];
+                m &= live;
+                if (!__any(m != 0)) continue;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    park[j * 64 + lane] = make_float4(acc[rb][h][4 * j], acc[rb][h][4 * j + 1],
+                                                      acc[rb][h][4 * j + 2], acc[rb][h][4 * j + 3]);
+                const float* pk = reinterpret_cast<const float*>(park);
+                while (__any(m != 0)) {
+                    if (m) {
+                        const int r = __builtin_ctz(m);
+                        m &= m - 1u;
+                        const float a = pk[((r >> 2) * 64 + lane) * 4 + (r & 3)];
+                        const int tr = rbase + (r & 3) + 8 * (r >> 2);
                         float kv;
                         if (L2) {
-                            kv = fmaf(-2.f, acc[rb][h][r], qn[h] + nv[i]);
+                            kv = fmaf(-2.f, a, qn[h] + nrm[tr]);
                             kv = kv < 0.f ? 0.f : kv;
                         } else {
-                            kv = -acc[rb][h][r];
+                            kv = -a;
                         }
-                        key[r] = kv;
-                        const bool pass = (full || row_ok(rbase + 8 * j + i)) && kv < tau &&
-                                          kv <= tau_p;
-                        mask |= (unsigned)pass << r;
-                    }
-                }
-                if (__any(mask != 0)) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) park[r * 64 + lane] = key[r];
-                    unsigned m = mask;
-                    while (__any(m != 0)) {
-                        if (m) {
-                            const int r = __builtin_ctz(m);
-                            m &= m - 1u;
-                            const float kv = park[r * 64 + lane];
-                            const int row = trow(t, rbase + (r & 3) + 8 * (r >> 2));
-                            if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, row);
-                        }
+                        if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
                     }
                 }
             }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
+            if (lh == 0) share[((wr * 4 + wq) * 2 + h) * 32 + li] = jb;
         }
         barrier_lds();                                          // parking done before refill
     }
