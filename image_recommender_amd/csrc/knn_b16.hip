@@ -11,17 +11,19 @@
 // (2·N·D·Q·(1/BM + 1/BQ)) and a 128-row x 64-query wave tile reads 0.75 KiB per MFMA.
 //
 // Geometry: 8 waves = 2 (rows) x 4 (queries), wave tile 128 rows x 64 queries = 4 x 2 blocks of
-// 32 x 32.  Stage = 64 bf16 of depth per row (128 B): A 256 rows + B 256 queries = 64 KiB, two
-// stages in flight (128 KiB + row norms).  Each wave moves 8 one-KiB pieces per stage (waves 0-3
-// the corpus tile, 4-7 the query tile) with global_load_lds_dwordx4 in the saddr form: one
-// per-piece 32-bit lane offset fixed for the whole launch, one scalar base per stage, one M0 write
-// per four pieces (instruction offsets).  Per stage: issue the next stage's DMA, four 16-deep
-// k-steps (fragments of step c+1 read while step c's 8 MFMAs run), wait for the own DMA, barrier.
-// Measured bound: the per-CU global->LDS rate (~25 B/clk; 64 KiB per stage against 2048 MFMA
-// cycles per SIMD) — spreading the DMA issue between k-steps did not help.  After a tile's last stage: barrier,
-// top-k epilogue (accumulators of rows that pass the screen parked in the just-consumed stage),
-// barrier.
-//
+// 32 x 32.  Stage = 64 bf16 of depth per row (128 B): A 256 rows + B 256 queries = 64 KiB, a
+// two-slot ring (128 KiB) + row norms, screen bounds and a per-wave park region (150 KiB).  Each
+// wave moves 8 one-KiB pieces per stage (waves 0-3 the corpus tile, 4-7 the query tile) with
+// global_load_lds_dwordx4 in the saddr form: one per-piece 32-bit lane offset fixed for the
+// whole launch, one scalar base per stage, one M0 write per four pieces (instruction offsets).
+// Per stage: k-steps 0..2 (fragments of step c+1 read while step c's 8 MFMAs run), wait for the
+// own DMA of the next stage, barrier, read the next stage's first fragments and issue the DMA of
+// the stage after it into the slot just read, k-step 3.  After a tile's last stage the top-k
+// epilogue runs without barriers (it touches no stage memory).
+// Measured (profiles/r01_ablation_*): MFMA + fragment reads alone 2.74 ms of 3.8 at 1M x 1024 x
+// 1968; the LDS-DMA traffic (64 KiB per stage against 2048 MFMA cycles per SIMD) adds ~0.65 ms
+// even when never waited for, the epilogue ~0.4 ms.
+
 // LDS image: row r of a stage, 16-B chunk c stored at chunk c ^ ((r >> 1) & 7) (two 128-B rows
 // per 256-B bank row); the XOR is applied on the DMA's per-lane global source offset, so every
 // ds_read_b128 lane group of 16 hits 16 distinct bank slots.
@@ -44,14 +46,9 @@
 
 #include "knn_kernels.h"
 
-// Stage depth (32-bit words per staged row: 32 = 64 bf16, 16 = 32 bf16) and LDS ring depth.
-// 32 x 2: one barrier per 64-deep stage, the next stage's DMA in flight during one stage;
-// 16 x 4: a barrier per 32-deep stage, DMA issued three stages ahead.
+// Stage depth in 32-bit words per staged row (32 = 64 bf16 per row and stage).
 #ifndef IMGREC_B16_BKW
 #define IMGREC_B16_BKW 32
-#endif
-#ifndef IMGREC_B16_RING
-#define IMGREC_B16_RING 2
 #endif
 #ifndef IMGREC_B16_QB_PER_XCD      // query blocks per XCD group (see the block map)
 #define IMGREC_B16_QB_PER_XCD 4
@@ -68,8 +65,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kNW = 8;                    // waves: 2 along rows x 4 along queries
 constexpr int kBM = kB16BigRows;          // 256 corpus rows per tile
 constexpr int kBQ = kB16BigQueries;       // 256 queries per workgroup
-constexpr int kBKW = IMGREC_B16_BKW;      // 32-bit words (2 bf16) per staged row: 16 or 32
-constexpr int kNS = IMGREC_B16_RING;      // stages in the LDS ring
+constexpr int kBKW = IMGREC_B16_BKW;      // 32-bit words (2 bf16) per staged row
+constexpr int kNS = 2;                    // stages in the LDS ring
 constexpr int kRowB = kBKW * 4;           // bytes per staged row
 constexpr int kCPR = kBKW / 4;            // 16-B chunks per staged row
 constexpr int kKS = kCPR / 2;             // 16-deep MFMA k-steps per stage (chunks per lane half)
@@ -83,12 +80,11 @@ constexpr int kLPW = (kBM + kBQ) / kRPP / kNW;   // pieces per wave per stage (8
 constexpr int kNormSlots = 4;             // row-norm ring (tiles)
 constexpr int kNormOff = kNS * kStage;
 constexpr int kShareOff = kNormOff + kNormSlots * kBM * 4;   // per (wave, query): screen bound
-constexpr int kLDS = kShareOff + kNW * 2 * 32 * 4;
-static_assert(kBKW == 16 || kBKW == 32, "stage depth");
+constexpr int kParkOff = kShareOff + kNW * 2 * 32 * 4;     // per wave: 8 accumulators per lane
+constexpr int kLDS = kParkOff + kNW * 64 * 8 * 4;
+static_assert(kBKW == 32, "stage depth: four 16-deep k-steps per stage");
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
-static_assert(kNW * 16 * 64 * 4 <= kStage, "epilogue parking must fit in one stage");
-static_assert(kNS >= 2 && kNS <= 4, "ring depth");
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
     return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
@@ -110,6 +106,18 @@ __device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, const ui
         : "=&s"(keep)
         : "v"(v[4 * h]), "v"(v[4 * h + 1]), "v"(v[4 * h + 2]), "v"(v[4 * h + 3]), "s"(sbase),
           "s"(__builtin_amdgcn_readfirstlane(lds0))
+        : "memory");
+}
+
+// One one-KiB piece (instruction offset OFF, as piece OFF / 1024 of a dma4x group).
+template <int OFF>
+__device__ __forceinline__ void dma1(const void* sbase, uint32_t lds0, uint32_t v) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2 offset:%4\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds0)), "n"(OFF)
         : "memory");
 }
 
@@ -212,21 +220,17 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const bool isA = wave < 4;
     const int pbase = (isA ? wave : wave - 4) * kLPW;          // first piece index in its tile
     const int prow = lane / kCPR, pchk = lane % kCPR;
-    // Per-piece lane offsets in bytes from the stage's scalar base, minus the instruction offset
-    // dma4x adds to piece j.  The base sits 4 KiB below the tile's first row (corpus) or the
-    // query block, so an offset stays >= 0 when a piece past the split's end is clamped to the
-    // tile's first group (ng = groups the tile holds).
+    // Per-piece lane offsets in bytes from the stage's scalar base (the tile's first row, or the
+    // query block), minus the instruction offset dma4x adds to piece j (>= 0: piece j starts at
+    // least j KiB in).  Corpus piece P of a tile = the split's group t * kGPT + P.
     uint32_t voff[kLPW];
-    auto set_voff = [&](int ng) __attribute__((always_inline)) {
 #pragma unroll
-        for (int j = 0; j < kLPW; ++j) {
-            const int P = pbase + j, r = P * kRPP + prow;          // r: LDS row of this lane
-            const int srow = isA ? (P < ng ? P * nsplit * kRPP : 0) + prow : r;
-            voff[j] = (uint32_t)srow * (uint32_t)(dw * 4) +
-                      16u * (uint32_t)(pchk ^ ((r / kRPB) % kCPR)) + 4096u - 1024u * (uint32_t)(j & 3);
-        }
-    };
-    set_voff(kGPT);
+    for (int j = 0; j < kLPW; ++j) {
+        const int P = pbase + j, r = P * kRPP + prow;              // r: LDS row of this lane
+        const int srow = isA ? P * nsplit * kRPP + prow : r;
+        voff[j] = (uint32_t)srow * (uint32_t)(dw * 4) + 16u * (uint32_t)(pchk ^ ((r / kRPB) % kCPR)) -
+                  1024u * (uint32_t)(j & 3);
+    }
     const uint32_t smem0 = lds_u32(smem);
     const uint32_t pdst = (uint32_t)((isA ? 0 : kSA) + pbase * 1024);
 
@@ -257,111 +261,121 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     // DMA of stage g into ring slot g % kNS (+ the tile's row norms with its first stage)
     auto issue = [&](int g) __attribute__((always_inline)) {
         const int it = t0 + g / nst, is = g - (g / nst) * nst;
-        if (isA && is == 0 && it == t1 - 1 && cnt - it * kGPT < kGPT) set_voff(cnt - it * kGPT);
         const uint32_t* src = (isA ? xh + (size_t)trow(it, 0) * dw : qblk) + is * kBKW;
-        const char* sbase = reinterpret_cast<const char*>(src) - 4096;
         const uint32_t dst = smem0 + (uint32_t)((g % kNS) * kStage) + pdst;
+        const int ng = (isA && it == t1 - 1) ? cnt - it * kGPT : kGPT;   // groups in the tile
+        if (pbase + kLPW <= ng || !isA) {
 #pragma unroll
-        for (int h = 0; h < kLPW / 4; ++h) dma4x(sbase, dst + 4096u * h, voff, h);
+            for (int h = 0; h < kLPW / 4; ++h) dma4x(src, dst + 4096u * h, voff, h);
+        } else {
+            // the split's last, partial tile: pieces past its groups are skipped (their LDS rows
+            // keep stale data; the epilogue masks those rows)
+#pragma unroll
+            for (int j = 0; j < kLPW; ++j)
+                if (pbase + j < ng) {
+                    const uint32_t d = dst + 4096u * (j / 4);
+                    switch (j & 3) {                            // constant once unrolled
+                        case 0: dma1<0>(src, d, voff[j]); break;
+                        case 1: dma1<1024>(src, d, voff[j]); break;
+                        case 2: dma1<2048>(src, d, voff[j]); break;
+                        default: dma1<3072>(src, d, voff[j]); break;
+                    }
+                }
+        }
         if (is == 0 && wave < 4)
             dma4_norm(xnorm + trow(it, wave * 64 + lane),
                       smem0 + (uint32_t)(kNormOff + ((it - t0) % kNormSlots) * kBM * 4 + wave * 256));
     };
-    // wait until this wave's DMA of stage g has landed, given stages <= gi were issued
-    auto wait_stage = [&](int g, int gi) __attribute__((always_inline)) {
-        const int newer = gi - g;                               // stages issued after g
-        if (newer >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * kLPW) : "memory");
-        else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kLPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    // ---- top-k epilogue of one tile.  Screen: a row can only matter if its key beats T = min(own
+    // K-th, the partner lane's K-th, max over the query's four lists of their J-th best) — four
+    // lists holding J >= KM/4 entries each at or below that max already give the union KM better
+    // entries; a dropped row ranks behind the folded list's last entry (merge floor).  The test
+    // runs on the accumulator: d = (|x|^2 (1/2 - 2^-20) + c) - acc with c = (|q|^2 - T)/2 -
+    // 2^-20 (|q|^2 + |T|) is negative iff the row passes (the 2^-20 terms keep fp32 rounding from
+    // rejecting a row the exact key would keep); two packed adds per pair of rows and one
+    // v_alignbit per row shift the sign bits into a 16-bit lane mask.  A lane's passing rows are
+    // then visited one per round through the wave's own LDS park region (eight accumulators per
+    // lane at a time), keyed and inserted.  Touches no stage memory: needs no barrier of its own.
+    constexpr int kJ = (KM + 3) / 4;
+    constexpr float kLo = 1.0f / 1048576.f;
+    float* const share = reinterpret_cast<float*>(smem + kShareOff);
+    float4* const park = reinterpret_cast<float4*>(smem + kParkOff) + wave * (2 * 64);   // own region
+    const float* const pk = reinterpret_cast<const float*>(park);
+
+    // fragments of k-step c of a stage (A: 4 row blocks, B: 2 query blocks)
+    auto read_frags = [&](const char* sb, int c, u32x4 (&fa)[4], u32x4 (&fb)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) fa[rb] = *reinterpret_cast<const u32x4*>(sb + aoff[c] + rb * 32 * kRowB);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) fb[h] = *reinterpret_cast<const u32x4*>(sb + aoff[c] + boff + h * 32 * kRowB);
+    };
+    auto mfma_step = [&](f32x16 (&acc)[4][2], const u32x4 (&fa)[4], const u32x4 (&fb)[2]) __attribute__((always_inline)) {
+#ifdef IMGREC_ABLATE_NO_MFMA
+        // ablation: fragments read and consumed, no matrix work
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) asm volatile("" ::"v"(fa[rb]));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) asm volatile("" ::"v"(fb[h]));
+        if (nq < 0)
+#endif
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+                acc[rb][h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                    __builtin_bit_cast(bf16x8, fa[rb]), __builtin_bit_cast(bf16x8, fb[h]), acc[rb][h], 0, 0, 0);
     };
 
-    int gi = -1;                                                // last stage issued
-    for (int p = 0; p < kNS - 1 && p < total; ++p) issue(++gi);
-    if (total > 0) {
-        wait_stage(0, gi);
-        barrier_lds();
-    }
-
+    u32x4 fa[2][4], fb[2][2];
     int g = 0;
+    // ---- main loop.  One barrier per stage, placed before the stage's last k-step: by then every
+    // wave has read the whole stage (its slot is refilled with stage g + 2 right after) and waited
+    // for its own DMA of stage g + 1, so the next stage's first fragments are read after the
+    // barrier while the last k-step's MFMAs run — the MFMA pipe does not drain at the barrier.
+    if (total > 0) {
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        if (total > 1) issue(1);
+        read_frags(smem, 0, fa[0], fb[0]);
+    }
     for (int t = t0; t < t1; ++t) {
         f32x16 acc[4][2];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int h = 0; h < 2; ++h) acc[rb][h] = (f32x16){0.f};
-
-        int buf = 0;
         for (int s = 0; s < nst; ++s, ++g) {
-            buf = g % kNS;
-            // stage g + kNS - 1 goes into the slot read during stage g - 1 (every wave passed the
-            // barrier that ended it)
-#ifdef IMGREC_ABLATE_NO_DMA
-            if (gi + 1 < total && s == 0) issue(++gi);          // ablation: norms + a stage per tile
-#else
-            if (gi + 1 < total) issue(++gi);
-#endif
-            const char* sb = smem + buf * kStage;
-            u32x4 fa[2][4], fb[2][2];
+            const char* sb = smem + (g & 1) * kStage;
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-                fa[0][rb] = *reinterpret_cast<const u32x4*>(sb + aoff[0] + rb * 32 * kRowB);
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                fb[0][h] = *reinterpret_cast<const u32x4*>(sb + aoff[0] + boff + h * 32 * kRowB);
-#pragma unroll
-            for (int c = 0; c < kKS; ++c) {
-                const int cur = c & 1, nxt = cur ^ 1;
-                if (c + 1 < kKS) {
-#pragma unroll
-                    for (int rb = 0; rb < 4; ++rb)
-                        fa[nxt][rb] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + rb * 32 * kRowB);
-#pragma unroll
-                    for (int h = 0; h < 2; ++h)
-                        fb[nxt][h] = *reinterpret_cast<const u32x4*>(sb + aoff[c + 1] + boff + h * 32 * kRowB);
-                }
-#ifdef IMGREC_ABLATE_NO_MFMA
-                // ablation: fragments read and consumed, no matrix work
-#pragma unroll
-                for (int rb = 0; rb < 4; ++rb) asm volatile("" ::"v"(fa[cur][rb]));
-#pragma unroll
-                for (int h = 0; h < 2; ++h) asm volatile("" ::"v"(fb[cur][h]));
-                if (nq < 0)
-#endif
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-#pragma unroll
-                    for (int rb = 0; rb < 4; ++rb)
-                        acc[rb][h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                            __builtin_bit_cast(bf16x8, fa[cur][rb]), __builtin_bit_cast(bf16x8, fb[cur][h]),
-                            acc[rb][h], 0, 0, 0);
+            for (int c = 0; c + 1 < kKS; ++c) {
+                read_frags(sb, c + 1, fa[(c + 1) & 1], fb[(c + 1) & 1]);
+                mfma_step(acc, fa[c & 1], fb[c & 1]);
             }
-            // own DMA of the next stage landed, own fragment reads done; then everyone's
+            // (the fences keep the compiler from sinking k-step kKS-2's MFMAs below the wait)
+            __builtin_amdgcn_sched_barrier(0);
 #ifdef IMGREC_ABLATE_NO_WAIT
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
-            if (g + 1 < total) wait_stage(g + 1, gi);
-            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
-            if (s + 1 < nst) barrier_lds();
+            __builtin_amdgcn_sched_barrier(0);
+            barrier_lds();
+            __builtin_amdgcn_sched_barrier(0);
+            // (after a tile's last stage the next fragments are read after the epilogue instead)
+            if (s + 1 < nst) read_frags(smem + ((g + 1) & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
+#ifdef IMGREC_ABLATE_NO_DMA
+            if (g + 2 < total && (g + 2) % nst == 0) issue(g + 2);   // ablation: norms + a stage per tile
+#else
+            if (g + 2 < total) issue(g + 2);
+#endif
+            mfma_step(acc, fa[(kKS - 1) & 1], fb[(kKS - 1) & 1]);
         }
-
-        // ---- epilogue.  Screen: a row can only matter if its key beats T = min(own K-th, the
-        // partner lane's K-th, max over the query's four lists of their J-th best) — four lists
-        // holding J >= KM/4 entries each at or below that max already give the union KM better
-        // entries; a dropped row ranks behind the folded list's last entry (merge floor).  The
-        // test runs on the accumulator: d = (|x|^2 (1/2 - 2^-20) + c) - acc with c = (|q|^2 -
-        // T)/2 - 2^-20 (|q|^2 + |T|) is negative iff the row passes (the 2^-20 terms keep fp32
-        // rounding from rejecting a row the exact key would keep); two packed adds per pair of
-        // rows and one v_alignbit per row shift the sign bits into a 16-bit lane mask.  Rows a
-        // lane passed: raw accumulators parked in the spent stage, keys computed, inserted.
-        barrier_lds();                                          // spent stage free for parking
+        // ---- epilogue of tile t (see above)
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
-        float* share = reinterpret_cast<float*>(smem + kShareOff);
-        float4* park = reinterpret_cast<float4*>(smem + buf * kStage) + wave * (4 * 64);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
-        constexpr int kJ = (KM + 3) / 4;
-        constexpr float kLo = 1.0f / 1048576.f;
         float cth[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -373,7 +387,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             const float other = share[(((1 - wr) * 4 + wq) * 2 + h) * 32 + li];
 #endif
             const float T = fminf(fminf(tau, __shfl_xor(tau, 32, 64)), fmaxf(jb, other));
-            float c = L2 ? 0.5f * (qn[h] - T) - kLo * (qn[h] + fabsf(T)) : -T;
+            const float c = L2 ? 0.5f * (qn[h] - T) - kLo * (qn[h] + fabsf(T)) : -T;
             cth[h] = qcol[h] < nq ? c : INFINITY;
         }
 #pragma unroll
@@ -409,38 +423,44 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                unsigned m = msk[h];
-                m &= live;
+                const unsigned m = msk[h] & live;
                 if (!__any(m != 0)) continue;
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    park[j * 64 + lane] = make_float4(acc[rb][h][4 * j], acc[rb][h][4 * j + 1],
-                                                      acc[rb][h][4 * j + 2], acc[rb][h][4 * j + 3]);
-                const float* pk = reinterpret_cast<const float*>(park);
-                while (__any(m != 0)) {
-                    if (m) {
-                        const int r = __builtin_ctz(m);
-                        m &= m - 1u;
-                        const float a = pk[((r >> 2) * 64 + lane) * 4 + (r & 3)];
-                        const int tr = rbase + (r & 3) + 8 * (r >> 2);
-                        float kv;
-                        if (L2) {
-                            kv = fmaf(-2.f, a, qn[h] + nrm[tr]);
-                            kv = kv < 0.f ? 0.f : kv;
-                        } else {
-                            kv = -a;
+                for (int hf = 0; hf < 2; ++hf) {                // rows 8hf .. 8hf+7 of the block
+                    unsigned mh = (m >> (8 * hf)) & 0xffu;
+                    if (!__any(mh != 0)) continue;
+                    park[lane] = make_float4(acc[rb][h][8 * hf], acc[rb][h][8 * hf + 1],
+                                             acc[rb][h][8 * hf + 2], acc[rb][h][8 * hf + 3]);
+                    park[64 + lane] = make_float4(acc[rb][h][8 * hf + 4], acc[rb][h][8 * hf + 5],
+                                                  acc[rb][h][8 * hf + 6], acc[rb][h][8 * hf + 7]);
+                    while (__any(mh != 0)) {
+                        if (mh) {
+                            const int r8 = __builtin_ctz(mh);
+                            mh &= mh - 1u;
+                            const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
+                            const int r = 8 * hf + r8;
+                            const int tr = rbase + (r & 3) + 8 * (r >> 2);
+                            float kv;
+                            if (L2) {
+                                kv = fmaf(-2.f, a, qn[h] + nrm[tr]);
+                                kv = kv < 0.f ? 0.f : kv;
+                            } else {
+                                kv = -a;
+                            }
+                            if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
                         }
-                        if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
                     }
                 }
             }
         }
+        // publish this wave's J-th bound per query (pair max) for the other row-half wave; a
+        // reader sees this or an older (larger) value: both bound the lists
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
             if (lh == 0) share[((wr * 4 + wq) * 2 + h) * 32 + li] = jb;
         }
-        barrier_lds();                                          // parking done before refill
+        if (g < total) read_frags(smem + (g & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
     }
 
     // ---- one list per (query, row split): fold the partner lane's list (lane ^ 32, the query's
