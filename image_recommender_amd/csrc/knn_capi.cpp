@@ -225,8 +225,9 @@ struct knn_index {
     uint32_t* qsplit = nullptr; size_t qsplit_cap = 0;
     float* cand2_d = nullptr; size_t cand2_d_cap = 0;
     int64_t* cand2_i = nullptr; size_t cand2_i_cap = 0;
-    int* fail = nullptr; size_t fail_cap = 0;          // [0] = count, [1..] = list
-    float* err_ratio = nullptr; size_t err_ratio_cap = 0;
+    // [0] = uncertified count, [1] = max observed error / bound (float bits), [2..] = their list
+    int* fail = nullptr; size_t fail_cap = 0;
+    int* hstat = nullptr;                               // pinned host copy of fail[0..1]
     float last_err_ratio = 0.f;
     uint16_t* qb16 = nullptr; size_t qb16_cap = 0;
     float* q_resid = nullptr; size_t q_resid_cap = 0;
@@ -406,6 +407,16 @@ bool use_split(const knn_index* ix, int64_t nq, int k) {
 int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
                 int64_t* I, hipStream_t st, bool timed);
 
+// Uncertified count and max error ratio of the last rerank: one 8-byte copy into pinned memory.
+int read_stats(knn_index* ix, hipStream_t st, int* nfail, float* ratio) {
+    if (!ix->hstat) KNN_HIP(hipHostMalloc((void**)&ix->hstat, 2 * sizeof(int), hipHostMallocDefault));
+    KNN_HIP(hipMemcpyAsync(ix->hstat, ix->fail, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    KNN_HIP(hipStreamSynchronize(st));
+    *nfail = ix->hstat[0];
+    std::memcpy(ratio, &ix->hstat[1], sizeof(float));
+    return KNN_OK;
+}
+
 // Re-run the nfail queries listed in `list` (device, indices into qpad) on the next, more precise
 // path — the split path when enough of them fail and it is available, else the exact kernel —
 // and scatter the results back into D, I.  Own workspace: the nested path may use every other.
@@ -450,8 +461,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 1)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->err_ratio, &ix->err_ratio_cap, 1)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 2)) != KNN_OK) return rc;
     if (!q_ready)   // else search_locked's fused query prep already wrote qb16 / q_resid
         KNN_HIP(imgrec::launch_bf16_rows(qpad, p.nq_pad, ix->dp, ix->dpb, ix->qb16, ix->q_resid, st));
     TileArgs a{};
@@ -473,27 +483,24 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
                                             ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
                                             ix->mws_d, ix->mws_i, ix->mws_f, st));
-    KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
-    KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
+    KNN_HIP(hipMemsetAsync(ix->fail, 0, 2 * sizeof(int), st));
     imgrec::RerankArgs r{};
     r.mode = imgrec::kModeBF16;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = b16_acc_coef(ix->dpb);
     r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I; r.fail_count = ix->fail;
-    r.fail_list = ix->fail + 1; r.err_ratio = ix->err_ratio;
+    r.fail_list = ix->fail + 2; r.err_ratio = reinterpret_cast<float*>(ix->fail + 1);
     r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
     KNN_HIP(imgrec::launch_rerank_certify(r, st));
     int nfail = 0;
     float ratio = 0.f;
-    KNN_HIP(hipMemcpyAsync(&nfail, ix->fail, sizeof(int), hipMemcpyDeviceToHost, st));
-    KNN_HIP(hipMemcpyAsync(&ratio, ix->err_ratio, sizeof(float), hipMemcpyDeviceToHost, st));
-    KNN_HIP(hipStreamSynchronize(st));
+    if ((rc = read_stats(ix, st, &nfail, &ratio)) != KNN_OK) return rc;
     ix->last_err_ratio = std::max(ix->last_err_ratio, ratio);
     ix->last_split_queries += nq;
     if (nfail <= 0) return KNN_OK;
     ix->last_fallback += nfail;
-    return cascade(ix, qpad, qnorm, ix->fail + 1, nfail, k, D, I, st);
+    return cascade(ix, qpad, qnorm, ix->fail + 2, nfail, k, D, I, st);
 }
 
 // Split-bf16 candidates + exact rerank + certificate; uncertified queries re-run exactly.
@@ -509,8 +516,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 1)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->err_ratio, &ix->err_ratio_cap, 1)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 2)) != KNN_OK) return rc;
     KNN_HIP(imgrec::launch_split_rows(qpad, p.nq_pad, ix->dp, imgrec::kSplitBK, ix->qsplit, st));
     TileArgs a{};
     a.wr = p.wr; a.wq = p.wq; a.km = kc;
@@ -527,22 +533,19 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     // global top-K' approximate candidates, raw ascending keys (merge in its L2 convention)
     KNN_HIP(imgrec::launch_merge(ix->cand_d, ix->cand_i, nq, a.ncand / kc, kc, a.ncand, kc, kc, 1,
                                  0, ix->cand2_d, ix->cand2_i, st));
-    KNN_HIP(hipMemsetAsync(ix->fail, 0, sizeof(int), st));
-    KNN_HIP(hipMemsetAsync(ix->err_ratio, 0, sizeof(float), st));
+    KNN_HIP(hipMemsetAsync(ix->fail, 0, 2 * sizeof(int), st));
     imgrec::RerankArgs r{};
     r.mode = imgrec::kModeSplit;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = split_coef(ix->dp);
     r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I; r.fail_count = ix->fail;
-    r.fail_list = ix->fail + 1;
-    r.err_ratio = ix->err_ratio;
+    r.fail_list = ix->fail + 2;
+    r.err_ratio = reinterpret_cast<float*>(ix->fail + 1);
     KNN_HIP(imgrec::launch_rerank_certify(r, st));
     int nfail = 0;
     float ratio = 0.f;
-    KNN_HIP(hipMemcpyAsync(&nfail, ix->fail, sizeof(int), hipMemcpyDeviceToHost, st));
-    KNN_HIP(hipMemcpyAsync(&ratio, ix->err_ratio, sizeof(float), hipMemcpyDeviceToHost, st));
-    KNN_HIP(hipStreamSynchronize(st));
+    if ((rc = read_stats(ix, st, &nfail, &ratio)) != KNN_OK) return rc;
     ix->last_err_ratio = std::max(ix->last_err_ratio, ratio);
     ix->last_split_queries += nq;
     if (nfail <= 0) return KNN_OK;
@@ -552,11 +555,11 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     if ((rc = grow(&ix->fb_qn, &ix->fb_qn_cap, (size_t)pf.nq_pad)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_d, &ix->fb_d_cap, (size_t)nfail * k)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_i, &ix->fb_i_cap, (size_t)nfail * k)) != KNN_OK) return rc;
-    KNN_HIP(imgrec::launch_gather_rows(qpad, qnorm, ix->dp, ix->fail + 1, nfail, pf.nq_pad, ix->fb_q,
+    KNN_HIP(imgrec::launch_gather_rows(qpad, qnorm, ix->dp, ix->fail + 2, nfail, pf.nq_pad, ix->fb_q,
                                        ix->fb_qn, st));
     if ((rc = exact_chunk(ix, ix->fb_q, ix->fb_qn, nfail, k, ix->fb_d, ix->fb_i, st, false)) != KNN_OK)
         return rc;
-    KNN_HIP(imgrec::launch_scatter_results(ix->fb_d, ix->fb_i, ix->fail + 1, nfail, k, D, I, st));
+    KNN_HIP(imgrec::launch_scatter_results(ix->fb_d, ix->fb_i, ix->fail + 2, nfail, k, D, I, st));
     return KNN_OK;
 }
 
@@ -674,10 +677,11 @@ int knn_free(knn_index_t* ix) {
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
                     (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,
-                    (void*)ix->qsplit, (void*)ix->cand2_d, (void*)ix->cand2_i, (void*)ix->fail, (void*)ix->err_ratio,
+                    (void*)ix->qsplit, (void*)ix->cand2_d, (void*)ix->cand2_i, (void*)ix->fail,
                     (void*)ix->fb_q, (void*)ix->fb_qn, (void*)ix->fb_d, (void*)ix->fb_i,
                     (void*)ix->hq, (void*)ix->hd, (void*)ix->hi})
         if (p) (void)hipFree(p);
+    if (ix->hstat) (void)hipHostFree(ix->hstat);
     for (hipEvent_t e : ix->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ix->stream);
     delete ix;

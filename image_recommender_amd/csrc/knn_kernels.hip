@@ -23,6 +23,7 @@
 // operands, so the contraction is unchanged).
 
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <float.h>
 #include <math.h>
@@ -730,14 +731,63 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
 
 // Candidate merge when every lane holds at most one sorted input list (<= 64 lists per query):
 // no insertion, the lane's list is its queue.  Entries are packed into one 64-bit value
-// (order-preserving key bits | local row), so each of the kout rounds is a 6-step u64 min
-// butterfly; the winning lane (unique: a row sits in one list) pops its head.
+// (order-preserving key bits | local row), so each of the kout rounds is one wave u64 minimum
+// (wave_min_u64); the winning lane (unique: a row sits in one list) pops its head.
 __device__ __forceinline__ uint32_t key_bits_ordered(float k) {
     const uint32_t u = __float_as_uint(k);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 __device__ __forceinline__ float key_from_ordered(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// Wave-wide minimum of a u64 with DPP row shifts (in-row prefix minimum, lanes shifting in from
+// outside the row keep the identity) and four lane reads: the result is uniform (SGPRs).  Replaces
+// a 6-step shuffle butterfly whose LDS-crossbar latency dominated the merge rounds.
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+    auto step = [&](auto ctrl) __attribute__((always_inline)) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)(uint32_t)v,
+                                                                  decltype(ctrl)::value, 0xf, 0xf, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)(uint32_t)(v >> 32),
+                                                                  decltype(ctrl)::value, 0xf, 0xf, false);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        v = o < v ? o : v;
+    };
+    step(std::integral_constant<int, 0x111>{});     // row_shr:1
+    step(std::integral_constant<int, 0x112>{});     // row_shr:2
+    step(std::integral_constant<int, 0x114>{});     // row_shr:4
+    step(std::integral_constant<int, 0x118>{});     // row_shr:8 -> lane 15 of a row: its minimum
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 16 * r + 15);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 16 * r + 15);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        m = o < m ? o : m;
+    }
+    return m;
+}
+
+// Wave-wide sum (uniform) and exclusive prefix sum of an int: DPP row_shr steps give the in-row
+// inclusive prefix, lane reads of the row totals carry it across rows.
+__device__ __forceinline__ int row_inclusive_sum(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    return x;
+}
+__device__ __forceinline__ int wave_sum_i32(int x) {
+    const int r = row_inclusive_sum(x);
+    return __builtin_amdgcn_readlane(r, 15) + __builtin_amdgcn_readlane(r, 31) +
+           __builtin_amdgcn_readlane(r, 47) + __builtin_amdgcn_readlane(r, 63);
+}
+__device__ __forceinline__ int wave_excl_scan_i32(int x) {
+    const int r = row_inclusive_sum(x);
+    const int t0 = __builtin_amdgcn_readlane(r, 15), t1 = __builtin_amdgcn_readlane(r, 31);
+    const int t2 = __builtin_amdgcn_readlane(r, 47);
+    const int row = (int)(threadIdx.x & 63) >> 4;
+    return r - x + (row > 0 ? t0 : 0) + (row > 1 ? t1 : 0) + (row > 2 ? t2 : 0);
 }
 
 // A query's nlists lists may be split into G groups of <= 64 (two-level merge): wave s handles
@@ -776,24 +826,57 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
     if (lane == 0) floor_out[sq] = fl;
-    for (int r = 0; r < kout; ++r) {
-        uint64_t b = v[0];
+
+    // Output = the K = min(kout, valid) smallest packed values.  T, the K-th smallest, is found
+    // bit by bit (count of entries <= a trial value, summed over the wave): 32 steps over the key
+    // bits, and the 32 row bits only when the K-th key is tied across the cut.  Each lane's
+    // entries <= T (a prefix of its sorted list) go to LDS slots from an exclusive scan; a lane's
+    // output position is its value's rank among the K (values are distinct: a row sits in one
+    // list).
+    auto count_le = [&](uint64_t x) __attribute__((always_inline)) {
+        int c = 0;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint32_t lo = __shfl_xor((uint32_t)b, off, 64);
-            const uint32_t hi = __shfl_xor((uint32_t)(b >> 32), off, 64);
-            const uint64_t o = ((uint64_t)hi << 32) | lo;
-            b = o < b ? o : b;
-        }
-        if (b != kEmpty && v[0] == b) {
+        for (int p = 0; p < KIN; ++p) c += v[p] <= x ? 1 : 0;
+        return c;
+    };
+    int nvl = 0;
 #pragma unroll
-            for (int p = 0; p < KIN - 1; ++p) v[p] = v[p + 1];
-            v[KIN - 1] = kEmpty;
+    for (int p = 0; p < KIN; ++p) nvl += v[p] != kEmpty ? 1 : 0;
+    const int K = min(kout, wave_sum_i32(nvl));
+    uint64_t T = 0;
+    if (K > 0) {
+        uint64_t prefix = 0;
+        for (int b = 63; b >= 32; --b) {
+            const uint64_t lo = prefix | ((1ull << b) - 1);
+            if (wave_sum_i32(count_le(lo)) < K) prefix |= 1ull << b;
         }
-        if (lane == 0) {
-            D[sq * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
-            I[sq * kout + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b + id_offset;
+        T = prefix | 0xffffffffull;
+        if (wave_sum_i32(count_le(T)) > K) {                   // the K-th key is tied: rows decide
+            for (int b = 31; b >= 0; --b) {
+                const uint64_t lo = prefix | ((1ull << b) - 1);
+                if (wave_sum_i32(count_le(lo)) < K) prefix |= 1ull << b;
+            }
+            T = prefix;
         }
+    }
+    __shared__ uint64_t sel[4][64];
+    uint64_t* buf = sel[threadIdx.x >> 6];
+    const int c = K > 0 ? count_le(T) : 0;
+    const int base = wave_excl_scan_i32(c);
+#pragma unroll
+    for (int p = 0; p < KIN; ++p)
+        if (p < c) buf[base + p] = v[p];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < K) {
+        const uint64_t mine = buf[lane];
+        int rank = 0;
+        for (int j = 0; j < K; ++j) rank += buf[j] < mine ? 1 : 0;
+        D[sq * kout + rank] = key_from_ordered((uint32_t)(mine >> 32));
+        I[sq * kout + rank] = (int64_t)(uint32_t)mine + id_offset;
+    } else if (lane < kout) {
+        D[sq * kout + lane] = FLT_MAX;
+        I[sq * kout + lane] = -1;
     }
 }
 
@@ -828,14 +911,7 @@ cand_merge_lds_kernel(const float* __restrict__ cd, const int64_t* __restrict__ 
     int head = 0;
     uint64_t cur = qv[lane * 65];
     for (int r = 0; r < kout; ++r) {
-        uint64_t b = cur;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint32_t lo = __shfl_xor((uint32_t)b, off, 64);
-            const uint32_t hi = __shfl_xor((uint32_t)(b >> 32), off, 64);
-            const uint64_t o = ((uint64_t)hi << 32) | lo;
-            b = o < b ? o : b;
-        }
+        const uint64_t b = wave_min_u64(cur);
         if (b != kEmpty && cur == b) cur = qv[lane * 65 + (++head)];
         if (lane == 0) {
             D[q * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));

@@ -8,7 +8,7 @@
 //   split_rows      fp32 rows -> split layout (per BK-deep stage j, lane half h and MFMA k-step
 //                   s < BK/16: a 16-B hi chunk and a 16-B lo chunk, logical chunks
 //                   h*(BK/8) + 2s and +1, holding depth BK*j + 16s + 8h + 0..7).
-//   rerank_certify  one wave per query: exact fp32 keys of the K' candidates (the same
+//   rerank_certify  one workgroup per query: exact fp32 keys of the K' candidates (the same
 //                   faiss exhaustive_L2sqr_blas key form as the exact kernel), top-k by
 //                   (key, label), and a certificate that no row outside the candidate set can
 //                   rank before a returned row:
@@ -190,9 +190,14 @@ __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
     return d1 < d2 || (d1 == d2 && i1 < i2);
 }
 
-// One wave per query.  cd/ci: the merged approximate candidates, nq x kc, ascending raw keys
-// (L2 distance or -ip), empty = label -1.
-__global__ void __launch_bounds__(256)
+// One workgroup of kRerankWaves waves per query.  cd/ci: the merged approximate candidates,
+// nq x kc, ascending raw keys (L2 distance or -ip), empty = label -1.
+// IT > 0: the query row sits in registers (IT float4 per lane, dp <= 256 IT) and every wave loads
+// its candidates' rows kRerankRows at a time, all loads in flight at once; IT = 0 streams the
+// query with the rows (any dp).
+constexpr int kRerankWaves = 8, kRerankRows = 2;
+template <int IT>
+__global__ void __launch_bounds__(kRerankWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
 rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qnorm, int dp,
                       const float* __restrict__ xb, const float* __restrict__ xn,
                       const float* __restrict__ xn_max, int64_t id_offset,
@@ -202,9 +207,8 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
                       int* __restrict__ fail_list, float* __restrict__ err_ratio, int mode,
                       const float* __restrict__ q_resid, const float* __restrict__ xr_max,
                       const float* __restrict__ floor) {
-    // one 4-wave workgroup per query: every wave reranks a quarter of the prefix, wave 0 ranks
-    // and certifies
     __shared__ float skey[64];
+    __shared__ int64_t slab[64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int64_t q = blockIdx.x;
@@ -248,39 +252,22 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
         m = __popcll(__ballot(valid && ak <= thr));
     }
 
-    // exact fp32 keys of the prefix: candidate c goes to wave c % 4, four per wave pass
-    // (independent row loads in flight; each candidate's sum has the same order wherever it runs)
+    // exact fp32 keys of the prefix: candidate c goes to wave c % kRerankWaves (each candidate's
+    // sum has the same order wherever it runs)
     const int n4 = dp / 4;
     const float4* q4 = reinterpret_cast<const float4*>(qv);
-    for (int c0 = wave; c0 < m; c0 += 16) {
-        const float4* r4[4];
-        float acc[4];
+    auto row_of = [&](int c) {
+        const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
+        const int hi32 = __shfl((int)(lab >> 32), c, 64);
+        const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
+        return reinterpret_cast<const float4*>(xb + (l - id_offset) * dp);
+    };
+    auto finish = [&](float (&acc)[kRerankRows], int c0) {
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const int c = min(c0 + 4 * v, m - 1);                // clamped: loads unconditional
-            const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
-            const int hi32 = __shfl((int)(lab >> 32), c, 64);
-            const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
-            r4[v] = reinterpret_cast<const float4*>(xb + (l - id_offset) * dp);
-            acc[v] = 0.f;
-        }
-#pragma unroll 4
-        for (int i = lane; i < n4; i += 64) {
-            const float4 a = q4[i];
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const float4 b = r4[v][i];
-                acc[v] = fmaf(a.x, b.x, acc[v]);
-                acc[v] = fmaf(a.y, b.y, acc[v]);
-                acc[v] = fmaf(a.z, b.z, acc[v]);
-                acc[v] = fmaf(a.w, b.w, acc[v]);
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < kRerankRows; ++v) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
-            const int c = c0 + 4 * v;
+            const int c = c0 + kRerankWaves * v;
             if (lane != c || c >= m) continue;                   // candidate c sits in lane c
             float kv;
             if (metric == 1) {
@@ -291,7 +278,66 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
             }
             skey[c] = kv;
         }
+    };
+    if constexpr (IT > 0) {
+        float4 qr[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = lane + 64 * it;
+            qr[it] = i < n4 ? q4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
+            const float4* r4[kRerankRows];
+            float acc[kRerankRows];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                r4[v] = row_of(min(c0 + kRerankWaves * v, m - 1));   // clamped: loads unconditional
+                acc[v] = 0.f;
+            }
+            float4 b[kRerankRows][IT];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v)
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const int i = lane + 64 * it;
+                    b[v][it] = i < n4 ? r4[v][i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+            for (int it = 0; it < IT; ++it)
+#pragma unroll
+                for (int v = 0; v < kRerankRows; ++v) {
+                    acc[v] = fmaf(qr[it].x, b[v][it].x, acc[v]);
+                    acc[v] = fmaf(qr[it].y, b[v][it].y, acc[v]);
+                    acc[v] = fmaf(qr[it].z, b[v][it].z, acc[v]);
+                    acc[v] = fmaf(qr[it].w, b[v][it].w, acc[v]);
+                }
+            finish(acc, c0);
+        }
+    } else {
+        for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
+            const float4* r4[kRerankRows];
+            float acc[kRerankRows];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                r4[v] = row_of(min(c0 + kRerankWaves * v, m - 1));
+                acc[v] = 0.f;
+            }
+#pragma unroll 4
+            for (int i = lane; i < n4; i += 64) {
+                const float4 a = q4[i];
+#pragma unroll
+                for (int v = 0; v < kRerankRows; ++v) {
+                    const float4 bb = r4[v][i];
+                    acc[v] = fmaf(a.x, bb.x, acc[v]);
+                    acc[v] = fmaf(a.y, bb.y, acc[v]);
+                    acc[v] = fmaf(a.z, bb.z, acc[v]);
+                    acc[v] = fmaf(a.w, bb.w, acc[v]);
+                }
+            }
+            finish(acc, c0);
+        }
     }
+    if (wave == 0 && lane < 64) slab[lane] = lab;
     __syncthreads();
     if (wave != 0) return;
     const float key = lane < m ? skey[lane] : INFINITY;
@@ -299,13 +345,8 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
     // rank of this lane's candidate inside the prefix by (key, label)
     const bool inP = lane < m;
     int rank = 0;
-    for (int i = 0; i < m; ++i) {
-        const float ok = __shfl(key, i, 64);
-        const int lo32 = __shfl((int)(lab & 0xffffffff), i, 64);
-        const int hi32 = __shfl((int)(lab >> 32), i, 64);
-        const int64_t ol = ((int64_t)hi32 << 32) | (uint32_t)lo32;
-        if (inP && ranks_before_r(ok, ol, key, lab)) ++rank;
-    }
+    for (int i = 0; i < m; ++i)
+        if (inP && ranks_before_r(skey[i], slab[i], key, lab)) ++rank;
     if (inP && rank < k) {
         D[q * k + rank] = (metric == 1) ? key : -key;
         I[q * k + rank] = lab;
@@ -394,10 +435,16 @@ hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
     if (a.kc > 64 || a.k > a.kc || a.dp % 4 != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(rerank_certify_kernel, dim3((unsigned)a.nq), dim3(256), 0, st,
-                       a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci, a.kc,
-                       a.nq, a.k, a.metric, a.c_split, a.c_fp, a.D, a.I, a.fail_count, a.fail_list,
-                       a.err_ratio, a.mode, a.q_resid, a.xr_max, a.floor);
+#define IMGREC_RERANK(ITV)                                                                          \
+    hipLaunchKernelGGL((rerank_certify_kernel<ITV>), dim3((unsigned)a.nq), dim3(kRerankWaves * 64), \
+                       0, st, a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci,   \
+                       a.kc, a.nq, a.k, a.metric, a.c_split, a.c_fp, a.D, a.I, a.fail_count,        \
+                       a.fail_list, a.err_ratio, a.mode, a.q_resid, a.xr_max, a.floor)
+    if (a.dp <= 512) IMGREC_RERANK(2);
+    else if (a.dp <= 1024) IMGREC_RERANK(4);
+    else if (a.dp <= 2048) IMGREC_RERANK(8);
+    else IMGREC_RERANK(0);
+#undef IMGREC_RERANK
     return hipGetLastError();
 }
 
