@@ -811,6 +811,28 @@ int knn_merge_device(const float* cD, const int64_t* cI, int nlists, int64_t nq,
     return KNN_OK;
 }
 
+int64_t knn_packed_bytes(int64_t nq, int k) {
+    if (nq < 0 || k <= 0) return KNN_EINVAL;
+    const int64_t n = nq * k;
+    return (n + (n & 1)) * 4 + n * 8;
+}
+
+int knn_merge_packed_device(const void* packed, int nlists, int64_t nq, int kin, int k, int metric,
+                            float* D, int64_t* I, void* stream) {
+    if (nlists <= 0 || kin <= 0 || nq < 0) KNN_FAIL(KNN_EINVAL, "bad merge shape");
+    if (k <= 0 || k > KNN_MAX_K) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K, k);
+    if (nq == 0) return KNN_OK;
+    if (!packed || !D || !I) KNN_FAIL(KNN_EINVAL, "NULL pointer");
+    const int64_t n = nq * kin, nf = n + (n & 1);
+    const float* cD = static_cast<const float*>(packed);
+    const int64_t* cI = reinterpret_cast<const int64_t*>(static_cast<const char*>(packed) + nf * 4);
+    const int kmetric = metric == KNN_METRIC_L2 ? 1 : 0;
+    // chunk = nf floats + n int64: nf + 2n floats, nf / 2 + n int64
+    KNN_HIP(imgrec::launch_merge_strided(cD, cI, nq, nlists, kin, kin, nf + 2 * n, nf / 2 + n, k,
+                                         kmetric, kmetric ? 0 : 1, D, I, (hipStream_t)stream));
+    return KNN_OK;
+}
+
 int knn_normalize_L2(float* x, int64_t n, int d) {
     if (n < 0 || d <= 0 || (n > 0 && !x)) KNN_FAIL(KNN_EINVAL, "bad array");
     // faiss fvec_renorm_L2: per row, nr = |x|^2; if nr > 0: x *= 1 / sqrt(nr).  The norm is

@@ -110,6 +110,10 @@ hipError_t launch_b16_big(const TileArgs& a, hipStream_t st);     // knn_b16.hip
 hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st);
+// launch_merge with a separate list stride for the labels (packed key|label buffers)
+hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
+                                int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
+                                int metric, int negate_in, float* D, int64_t* I, hipStream_t st);
 // Candidate merge for the rerank: nq x kout approximate candidates (ascending raw keys, empty =
 // label -1) and, per query, the floor: the smallest key a row dropped by any list or by the merge's
 // own lane lists can have (+inf when nothing was dropped).

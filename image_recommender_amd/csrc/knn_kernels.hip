@@ -557,8 +557,8 @@ __device__ __forceinline__ void wave_select(float (&kd)[KM], int64_t (&ki)[KM], 
 template <int KM, int WPQ>
 __global__ void __launch_bounds__(256)
 knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
-                 int nlists, int kin, int64_t stride_q, int64_t stride_l, int k, int metric,
-                 int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
+                 int nlists, int kin, int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
+                 int metric, int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
                  float* __restrict__ floor_out) {
     constexpr int QPB = 4 / WPQ;                     // queries per 256-thread block
     __shared__ float sd[4][KM];
@@ -581,7 +581,7 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
     if (active) {
         for (int l = sub * 64 + lane; l < nlists; l += 64 * WPQ) {
             const float* lp = cd + q * stride_q + (int64_t)l * stride_l;
-            const int64_t* ip = ci + q * stride_q + (int64_t)l * stride_l;
+            const int64_t* ip = ci + q * stride_q + (int64_t)l * stride_li;
             if (floor_out && ip[kin - 1] >= 0) floor_v = fminf(floor_v, lp[kin - 1]);
             bool stop = false;
             for (int p0 = 0; p0 < kin && !stop; p0 += 8) {
@@ -706,6 +706,13 @@ hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
 hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st) {
+    return launch_merge_strided(cd, ci, nq, nlists, kin, stride_q, stride_l, stride_l, k, metric,
+                                negate_in, D, I, st);
+}
+
+hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
+                                int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
+                                int metric, int negate_in, float* D, int64_t* I, hipStream_t st) {
     if (nq <= 0) return hipSuccess;
     // few queries with many lists: 4 waves per query; otherwise one wave per query
     const bool wide = nq < 1024 && nlists > 256;
@@ -715,10 +722,10 @@ hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlis
     do {                                                                                            \
         if (wide)                                                                                   \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, k, metric, negate_in, D, I, nullptr);      \
+                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr);      \
         else                                                                                        \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 1>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, k, metric, negate_in, D, I, nullptr);      \
+                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr);      \
     } while (0)
     if (k <= 8) IMGREC_LAUNCH_MERGE(8);
     else if (k <= 10) IMGREC_LAUNCH_MERGE(10);
@@ -955,7 +962,7 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
     // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is
     // covered by the floor), the output takes kout rounds of the wave argmin
     hipLaunchKernelGGL((knn_merge_kernel<16, 1>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
-                       cd, ci, nq, nlists, kin, stride_q, stride_l, kout, 1, 0, D, I, floor);
+                       cd, ci, nq, nlists, kin, stride_q, stride_l, stride_l, kout, 1, 0, D, I, floor);
     return hipGetLastError();
 }
 

@@ -4,7 +4,8 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  The c
 into contiguous row ranges, rank r owning global labels [r*N/G, (r+1)*N/G) — the offsets table of
 the reference (main/create_index.py:236-249) is unchanged by sharding.  A search runs the fused
 kernel on every shard (labels already global via knn_set_id_offset), all-gathers the per-shard
-(nq, k) results (nq*k*12 bytes per rank: latency-bound, far below one xGMI link) and merges the
+(nq, k) results in one collective (keys and labels packed in one chunk, nq*k*12 bytes per rank:
+latency-bound, far below one xGMI link) and merges the
 G*k candidates per query with the same (key, label) order as a single-GPU search, so sharded and
 unsharded results are identical.
 
@@ -57,6 +58,52 @@ def merge_gathered_device(gD, gI, k: int, metric: int = METRIC_L2, stream: int =
     return D, I
 
 
+def packed_layout(nq: int, k: int) -> tuple[int, int]:
+    """(bytes per shard chunk, byte offset of the labels) of the packed key|label layout
+    (include/imgrec_knn.h knn_packed_bytes): nq*k float keys padded to an even count, then the
+    nq*k int64 labels."""
+    n = nq * k
+    off = 4 * (n + (n & 1))
+    return off + 8 * n, off
+
+
+def packed_views(buf, nq: int, k: int):
+    """(D, I) views (nq, k) of one packed chunk (uint8 tensor of packed_layout bytes)."""
+    import torch
+    nbytes, off = packed_layout(nq, k)
+    D = buf[:4 * nq * k].view(torch.float32).view(nq, k)
+    I = buf[off:nbytes].view(torch.int64).view(nq, k)
+    return D, I
+
+
+def gather_packed(buf, group=None):
+    """All-gather of every rank's packed chunk in ONE collective -> (world, nbytes) uint8."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    g = torch.empty((world, buf.numel()), dtype=torch.uint8, device=buf.device)
+    if world == 1:
+        g[0].copy_(buf)
+    elif dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(g, buf, group=group)
+    else:   # gloo (CPU tests): list form
+        dist.all_gather(list(g.unbind(0)), buf, group=group)
+    return g
+
+
+def merge_packed_device(g, nq: int, kin: int, k: int, metric: int = METRIC_L2, stream: int = 0):
+    """HIP merge (knn_merge_packed_device) of gathered packed chunks (world, nbytes) -> (nq, k)."""
+    import torch
+    world = g.shape[0]
+    D = torch.empty((nq, k), dtype=torch.float32, device=g.device)
+    I = torch.empty((nq, k), dtype=torch.int64, device=g.device)
+    _lib.check(_lib.load().knn_merge_packed_device(
+        C.c_void_p(g.data_ptr()), int(world), int(nq), int(kin), int(k), _METRIC_TO_KNN[metric],
+        C.c_void_p(D.data_ptr()), C.c_void_p(I.data_ptr()), C.c_void_p(stream or None)),
+        "knn_merge_packed_device")
+    return D, I
+
+
 class ShardedIndex:
     """This rank's shard of a row-partitioned exact index, plus the collective search."""
 
@@ -94,10 +141,14 @@ class ShardedIndex:
         import torch
         nq = q.shape[0]
         st = torch.cuda.current_stream(q.device).cuda_stream
-        D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
-        I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
-        self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
         if self.world == 1:
+            D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+            I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+            self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
             return D, I
-        gD, gI = gather_results(D, I, self.group)
-        return merge_gathered_device(gD, gI, k, self.metric, st)
+        # the shard searches straight into its packed chunk; one all-gather moves keys and labels
+        buf = torch.empty(packed_layout(nq, k)[0], dtype=torch.uint8, device=q.device)
+        D, I = packed_views(buf, nq, k)
+        self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
+        g = gather_packed(buf, self.group)
+        return merge_packed_device(g, nq, k, k, self.metric, st)

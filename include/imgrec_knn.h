@@ -17,14 +17,18 @@
  *   knn_read                             faiss.read_index(f)           main/search_from_image.py:339
  *   knn_normalize_L2                     faiss.normalize_L2(x)         main/search_from_image.py:322
  *   knn_merge_device                     (new) per-shard top-k merge after the RCCL all-gather (§8e)
+ *   knn_packed_bytes / knn_merge_packed_device  (new) the same over one packed key|label buffer,
+ *                                        so the all-gather is a single collective
  *
  * Conventions
  *   - All functions return 0 on success and a negative KNN_E* code on failure; the message of the
  *     last failure on the calling thread is returned by knn_last_error().
  *   - Host-pointer functions (knn_add, knn_search, knn_write, ...) synchronise before returning.
  *     *_device functions take device pointers and a hipStream_t (passed as void*; NULL = the
- *     HIP null stream, like any HIP API), enqueue asynchronously and never synchronise or allocate when the
- *     workspace is already large enough (so a caller may capture them into a hipGraph).
+ *     HIP null stream, like any HIP API) and enqueue asynchronously; they allocate only when the
+ *     workspace must grow.  knn_search_device synchronises its stream once per call on the
+ *     candidate paths (bf16 / split): the host reads the uncertified-query count (8 bytes) to
+ *     decide the re-run; the exact path never synchronises.
  *   - Vectors are row-major float32, n rows × d.  Labels are int64.  Result rows are sorted by
  *     ascending distance (L2) or descending inner product (IP/COSINE); exact ties are broken by the
  *     smaller label.  When fewer than k vectors exist, the tail of a result row holds label -1 and
@@ -116,6 +120,14 @@ int knn_search_device(knn_index_t* index, const float* q_dev, int64_t nq, int k,
  * label -1 are ignored.  Output nq*k, same ordering/padding rules as knn_search. */
 int knn_merge_device(const float* cand_D, const int64_t* cand_I, int nlists, int64_t nq, int kin,
                      int k, int metric, float* D_dev, int64_t* I_dev, void* stream);
+
+/* Packed per-shard results: one chunk of knn_packed_bytes(nq, k) bytes per shard holding the nq*k
+ * float keys (padded to an even count), then the nq*k int64 labels (8-byte aligned).  A shard
+ * searches straight into its chunk (D = chunk, I = chunk + 4 * (nq*k rounded up to even)); one
+ * all-gather of the chunks gives knn_merge_packed_device its [nlists] chunks. */
+int64_t knn_packed_bytes(int64_t nq, int k);
+int knn_merge_packed_device(const void* packed, int nlists, int64_t nq, int kin, int k, int metric,
+                            float* D_dev, int64_t* I_dev, void* stream);
 
 /* faiss IndexFlat on-disk layout ("IxF2" for L2, "IxFI" for IP/COSINE). */
 int knn_write(const knn_index_t* index, const char* path);

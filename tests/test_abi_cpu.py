@@ -121,3 +121,15 @@ def test_normalize_L2_host_entry():
     v = x[0].copy()
     faiss.normalize_L2(v)
     np.testing.assert_allclose(v, x[0] / n[0], rtol=3e-7)
+
+
+def test_packed_layout_matches_library():
+    """sharded.packed_layout (the Python views) and knn_packed_bytes (the merge's reading of the
+    chunk) agree, odd nq*k included; bad shapes are rejected."""
+    from image_recommender_amd.sharded import packed_layout
+    lib = _lib.load()
+    for nq, k in [(1, 1), (3, 3), (7, 10), (1024, 10), (5, 32)]:
+        nbytes, off = packed_layout(nq, k)
+        assert lib.knn_packed_bytes(nq, k) == nbytes
+        assert off % 8 == 0 and off >= 4 * nq * k and nbytes - off == 8 * nq * k
+    assert lib.knn_packed_bytes(-1, 3) < 0 and lib.knn_packed_bytes(3, 0) < 0

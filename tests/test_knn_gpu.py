@@ -236,6 +236,42 @@ def test_sharded_merge_is_bit_identical(faiss, mode, metric, shards, nq, k):
     np.testing.assert_array_equal(D.cpu().numpy(), Df)
 
 
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+@pytest.mark.parametrize("shards,nq,k", [(2, 7, 10), (4, 301, 5), (3, 1024, 10), (8, 1, 3)])
+def test_packed_merge_matches_gathered(faiss, metric, shards, nq, k):
+    """ShardedIndex.search's single-collective layout: each shard searches into its packed chunk
+    (keys, padding when nq*k is odd, labels) and knn_merge_packed_device gives exactly what
+    knn_merge_device gives on the separate [shards][nq][k] arrays."""
+    import torch
+    from image_recommender_amd.sharded import (merge_gathered_device, merge_packed_device,
+                                               packed_layout, packed_views, shard_range)
+    n, d = 6000, 96
+    xb = mixture(n, d, centres=40, seed=shards + nq)
+    xq = mixture(nq, d, centres=40, seed=nq + 3)
+    M = faiss.METRIC_L2 if metric == "l2" else faiss.METRIC_INNER_PRODUCT
+    nbytes = packed_layout(nq, k)[0]
+    g = torch.zeros((shards, nbytes), dtype=torch.uint8, device="cuda")
+    gD = torch.empty((shards, nq, k), dtype=torch.float32, device="cuda")
+    gI = torch.empty((shards, nq, k), dtype=torch.int64, device="cuda")
+    q = torch.from_numpy(xq).cuda()
+    for r in range(shards):
+        r0, r1 = shard_range(n, r, shards)
+        sh = faiss.IndexFlat(d, M)
+        sh.set_id_offset(r0)
+        sh.add(xb[r0:r1])
+        sh.search_mode = "exact"
+        pD, pI = packed_views(g[r], nq, k)
+        sh.search_device(q.data_ptr(), nq, k, pD.data_ptr(), pI.data_ptr(), 0)
+        sh.search_device(q.data_ptr(), nq, k, gD[r].data_ptr(), gI[r].data_ptr(), 0)
+        torch.cuda.synchronize()
+    D1, I1 = merge_gathered_device(gD, gI, k, M)
+    D2, I2 = merge_packed_device(g, nq, k, k, M)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(I2.cpu().numpy(), I1.cpu().numpy())
+    np.testing.assert_array_equal(D2.cpu().numpy(), D1.cpu().numpy())
+    check_knn(D2.cpu().numpy(), I2.cpu().numpy(), xb, xq, k, metric)
+
+
 def test_merge_device_padding_and_partial_lists(faiss):
     """Shards smaller than k: -1 tails in the gathered lists are skipped, output padded."""
     import torch
