@@ -76,12 +76,13 @@ def packed_views(buf, nq: int, k: int):
     return D, I
 
 
-def gather_packed(buf, group=None):
+def gather_packed(buf, group=None, out=None):
     """All-gather of every rank's packed chunk in ONE collective -> (world, nbytes) uint8."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    g = torch.empty((world, buf.numel()), dtype=torch.uint8, device=buf.device)
+    g = out if out is not None else torch.empty((world, buf.numel()), dtype=torch.uint8,
+                                                device=buf.device)
     if world == 1:
         g[0].copy_(buf)
     elif dist.get_backend(group) == "nccl":
@@ -121,6 +122,7 @@ class ShardedIndex:
         self.index = Index(d, metric, dev)
         self.index.set_id_offset(self.row0)
         self.index.reserve(self.row1 - self.row0)
+        self._packed = {}
 
     @property
     def local_rows(self) -> int:
@@ -147,8 +149,13 @@ class ShardedIndex:
             self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
             return D, I
         # the shard searches straight into its packed chunk; one all-gather moves keys and labels
-        buf = torch.empty(packed_layout(nq, k)[0], dtype=torch.uint8, device=q.device)
-        D, I = packed_views(buf, nq, k)
+        # (chunk and gather buffers are kept per (nq, k): every call is stream-ordered on them)
+        key = (nq, k, q.device)
+        if key not in self._packed:
+            buf = torch.empty(packed_layout(nq, k)[0], dtype=torch.uint8, device=q.device)
+            g = torch.empty((self.world, buf.numel()), dtype=torch.uint8, device=q.device)
+            self._packed = {key: (buf, g) + packed_views(buf, nq, k)}
+        buf, g, D, I = self._packed[key]
         self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
-        g = gather_packed(buf, self.group)
+        gather_packed(buf, self.group, out=g)
         return merge_packed_device(g, nq, k, k, self.metric, st)
