@@ -55,6 +55,13 @@
 #endif
 
 namespace imgrec {
+#ifdef IMGREC_B16_PROF
+// Debug build only (tools/prof_b16.py): per-wave cycle and event counts, summed over waves.
+__device__ unsigned long long g_b16prof[8];
+#define B16_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#else
+#define B16_T(v)
+#endif
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -93,8 +100,8 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 // Four one-KiB LDS-DMA pieces under ONE M0 value: the instruction offset (j KiB) moves both the
 // global source and the LDS destination (measured, tools/micro/glds_offset.hip), so the per-lane
 // offsets v[j] are pre-reduced by j KiB.
-template <int N>
-__device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, const uint32_t (&v)[N], int h) {
+__device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, uint32_t v0, uint32_t v1,
+                                      uint32_t v2, uint32_t v3) {
     unsigned keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
@@ -104,8 +111,7 @@ __device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, const ui
         "global_load_lds_dwordx4 %4, %5 offset:3072\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(v[4 * h]), "v"(v[4 * h + 1]), "v"(v[4 * h + 2]), "v"(v[4 * h + 3]), "s"(sbase),
-          "s"(__builtin_amdgcn_readfirstlane(lds0))
+        : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds0))
         : "memory");
 }
 
@@ -227,15 +233,21 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int prow = lane / kCPR, pchk = lane % kCPR;
     // Per-piece lane offsets in bytes from the stage's scalar base (the tile's first row, or the
     // query block), minus the instruction offset dma4x adds to piece j (>= 0: piece j starts at
-    // least j KiB in).  Corpus piece P of a tile = the split's group t * kGPT + P.
-    uint32_t voff[kLPW];
+    // least j KiB in).  Corpus piece P of a tile = the split's group t * kGPT + P.  Pieces are
+    // kPS bytes apart and the swizzle of a piece's rows depends only on the piece's parity, so
+    // the lane keeps two bases and piece j's offset is vpar[j & 1] + j * kPS - 1024 (j & 3).
+    static_assert(kRPP == 8 && kRPB == 2 && kCPR == 8 && kLPW % 2 == 0, "piece offset form");
+    uint32_t vpar[2];
 #pragma unroll
-    for (int j = 0; j < kLPW; ++j) {
-        const int P = pbase + j, r = P * kRPP + prow;              // r: LDS row of this lane
+    for (int e = 0; e < 2; ++e) {
+        const int P = pbase + e, r = P * kRPP + prow;              // r: LDS row of this lane
         const int srow = isA ? P * nsplit * kRPP + prow : r;
-        voff[j] = (uint32_t)srow * (uint32_t)(dw * 4) + 16u * (uint32_t)(pchk ^ ((r / kRPB) % kCPR)) -
-                  1024u * (uint32_t)(j & 3);
+        vpar[e] = (uint32_t)srow * (uint32_t)(dw * 4) + 16u * (uint32_t)(pchk ^ ((r / kRPB) % kCPR));
     }
+    const uint32_t kPS = (uint32_t)((isA ? nsplit : 1) * kRPP * dw * 4);   // bytes between pieces
+    auto voff_of = [&](int j) {
+        return vpar[j & 1] + (uint32_t)(j & ~1) * kPS - 1024u * (uint32_t)(j & 3);
+    };
     const uint32_t smem0 = lds_u32(smem);
     const uint32_t pdst = (uint32_t)((isA ? 0 : kSA) + pbase * 1024);
 
@@ -271,7 +283,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         const int ng = (isA && it == t1 - 1) ? cnt - it * kGPT : kGPT;   // groups in the tile
         if (pbase + kLPW <= ng || !isA) {
 #pragma unroll
-            for (int h = 0; h < kLPW / 4; ++h) dma4x(src, dst + 4096u * h, voff, h);
+            for (int h = 0; h < kLPW / 4; ++h)
+                dma4x(src, dst + 4096u * h, voff_of(4 * h), voff_of(4 * h + 1), voff_of(4 * h + 2),
+                      voff_of(4 * h + 3));
         } else {
             // the split's last, partial tile: pieces past its groups are skipped (their LDS rows
             // keep stale data; the epilogue masks those rows)
@@ -280,10 +294,10 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                 if (pbase + j < ng) {
                     const uint32_t d = dst + 4096u * (j / 4);
                     switch (j & 3) {                            // constant once unrolled
-                        case 0: dma1<0>(src, d, voff[j]); break;
-                        case 1: dma1<1024>(src, d, voff[j]); break;
-                        case 2: dma1<2048>(src, d, voff[j]); break;
-                        default: dma1<3072>(src, d, voff[j]); break;
+                        case 0: dma1<0>(src, d, voff_of(j)); break;
+                        case 1: dma1<1024>(src, d, voff_of(j)); break;
+                        case 2: dma1<2048>(src, d, voff_of(j)); break;
+                        default: dma1<3072>(src, d, voff_of(j)); break;
                     }
                 }
         }
@@ -345,7 +359,12 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         if (total > 1) issue(1);
         read_frags(smem, 0, fa[0], fb[0]);
     }
+#ifdef IMGREC_B16_PROF
+    unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    B16_T(tk0);
+#endif
     for (int t = t0; t < t1; ++t) {
+        B16_T(tl0);
         f32x16 acc[4][2];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
@@ -378,6 +397,10 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             mfma_step(acc, fa[(kKS - 1) & 1], fb[(kKS - 1) & 1]);
         }
         // ---- epilogue of tile t (see above)
+        B16_T(te0);
+#ifdef IMGREC_B16_PROF
+        pr[5] += te0 - tl0;
+#endif
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
@@ -430,6 +453,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             for (int h = 0; h < 2; ++h) {
                 const unsigned m = msk[h] & live;
                 if (!__any(m != 0)) continue;
+#ifdef IMGREC_B16_PROF
+                pr[6] += t == t0 ? 0 : 1;
+#endif
 #pragma unroll
                 for (int hf = 0; hf < 2; ++hf) {                // rows 8hf .. 8hf+7 of the block
                     unsigned mh = (m >> (8 * hf)) & 0xffu;
@@ -439,6 +465,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     park[64 + lane] = make_float4(acc[rb][h][8 * hf + 4], acc[rb][h][8 * hf + 5],
                                                   acc[rb][h][8 * hf + 6], acc[rb][h][8 * hf + 7]);
                     while (__any(mh != 0)) {
+#ifdef IMGREC_B16_PROF
+                        pr[t == t0 ? 3 : 4] += 1;
+#endif
                         if (mh) {
                             const int r8 = __builtin_ctz(mh);
                             mh &= mh - 1u;
@@ -465,8 +494,23 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
             if (lh == 0) share[((wr * 4 + wq) * 2 + h) * 32 + li] = jb;
         }
+#ifdef IMGREC_B16_PROF
+        {
+            B16_T(te1);
+            pr[t == t0 ? 0 : 1] += te1 - te0;
+            pr[7] += 1;
+        }
+#endif
         if (g < total) read_frags(smem + (g & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
     }
+#ifdef IMGREC_B16_PROF
+    {
+        B16_T(tk1);
+        pr[2] = tk1 - tk0;
+        if (lane == 0)
+            for (int i = 0; i < 8; ++i) atomicAdd(&g_b16prof[i], pr[i]);
+    }
+#endif
 
     // ---- one list per (query, row split): fold the partner lane's list (lane ^ 32, the query's
     // other rows) by shuffles, then wave wr = 1's lists into wave wr = 0's through LDS.  Entries a
@@ -537,3 +581,13 @@ hipError_t launch_b16_big(const TileArgs& a, hipStream_t st) {
 }
 
 }  // namespace imgrec
+
+#ifdef IMGREC_B16_PROF
+extern "C" int knn_debug_b16prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(imgrec::g_b16prof), 8 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -2;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(imgrec::g_b16prof), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
