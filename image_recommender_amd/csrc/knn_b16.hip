@@ -145,16 +145,18 @@ __device__ __forceinline__ void barrier_lds() {
 // behind the entries already present (ties by smaller label).
 template <int K>
 __device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float d, int id) {
+    // c[p]: d goes before slot p (on the old list; monotone in p).  Slot p takes slot p-1's entry
+    // when d goes before p-1, else d when it goes before p: one compare, four selects per slot.
+    bool c[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) c[p] = d < kd[p];
 #pragma unroll
     for (int p = K - 1; p > 0; --p) {
-        const bool shift = d < kd[p - 1];
-        const bool here = !shift && d < kd[p];
-        kd[p] = shift ? kd[p - 1] : (here ? d : kd[p]);
-        ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
+        kd[p] = c[p - 1] ? kd[p - 1] : (c[p] ? d : kd[p]);
+        ki[p] = c[p - 1] ? ki[p - 1] : (c[p] ? id : ki[p]);
     }
-    const bool here0 = d < kd[0];
-    kd[0] = here0 ? d : kd[0];
-    ki[0] = here0 ? id : ki[0];
+    kd[0] = c[0] ? d : kd[0];
+    ki[0] = c[0] ? id : ki[0];
 }
 
 // (d1, i1) ranks before (d2, i2): smaller key, ties by smaller label (empty = label -1 last).
@@ -452,10 +454,24 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const unsigned m = msk[h] & live;
+#ifdef IMGREC_ABLATE_SCREEN_ONLY
+                asm volatile("" ::"v"(m));
+                continue;
+#endif
                 if (!__any(m != 0)) continue;
 #ifdef IMGREC_B16_PROF
                 pr[6] += t == t0 ? 0 : 1;
 #endif
+                auto key_of = [&](float a, int tr) __attribute__((always_inline)) {
+                    float kv;
+                    if (L2) {
+                        kv = fmaf(-2.f, a, qn[h] + nrm[tr]);
+                        kv = kv < 0.f ? 0.f : kv;
+                    } else {
+                        kv = -a;
+                    }
+                    return kv;
+                };
 #pragma unroll
                 for (int hf = 0; hf < 2; ++hf) {                // rows 8hf .. 8hf+7 of the block
                     unsigned mh = (m >> (8 * hf)) & 0xffu;
@@ -474,13 +490,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                             const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
                             const int r = 8 * hf + r8;
                             const int tr = rbase + (r & 3) + 8 * (r >> 2);
-                            float kv;
-                            if (L2) {
-                                kv = fmaf(-2.f, a, qn[h] + nrm[tr]);
-                                kv = kv < 0.f ? 0.f : kv;
-                            } else {
-                                kv = -a;
-                            }
+                            const float kv = key_of(a, tr);
                             if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
                         }
                     }

@@ -7,7 +7,7 @@ import ctypes as C
 import os
 import sys
 
-os.environ["IMGREC_LIB_NAME"] = "libimgrec_b16prof.so"
+os.environ.setdefault("IMGREC_LIB_NAME", "libimgrec_b16prof.so")
 rows = sys.argv[1] if len(sys.argv) > 1 else "1000000"
 sys.argv = [sys.argv[0], "--profile-only", "--steps", "1", "--warmup", "0", "--rows", rows]
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
