@@ -200,16 +200,17 @@ __device__ __forceinline__ void barrier_raw() {
 // key comparison and an equal key always lands behind the existing entries.
 template <int K>
 __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], float d, int id) {
+    // c[p]: d goes before slot p of the old list (monotone); one compare, four selects per slot
+    bool c[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) c[p] = d < kd[p];
 #pragma unroll
     for (int p = K - 1; p > 0; --p) {
-        const bool shift = d < kd[p - 1];
-        const bool here = !shift && d < kd[p];
-        kd[p] = shift ? kd[p - 1] : (here ? d : kd[p]);
-        ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
+        kd[p] = c[p - 1] ? kd[p - 1] : (c[p] ? d : kd[p]);
+        ki[p] = c[p - 1] ? ki[p - 1] : (c[p] ? id : ki[p]);
     }
-    const bool here0 = d < kd[0];
-    kd[0] = here0 ? d : kd[0];
-    ki[0] = here0 ? id : ki[0];
+    kd[0] = c[0] ? d : kd[0];
+    ki[0] = c[0] ? id : ki[0];
 }
 
 // 4-wave workgroups run two per CU (two waves per SIMD): hold them to 256 VGPR+AGPR per lane.
