@@ -197,7 +197,10 @@ def pmc_traffic(pattern: str):
     import glob
     import re
     pat = re.compile(pattern)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    def version(f):                                  # r01_v13_traffic.json -> (1, 13)
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=version)
     for f in reversed(files):
         try:
             data = json.load(open(f))
