@@ -191,6 +191,27 @@ def kernel_pattern(tile_rows: int, tile_queries: int, path: int, k: int):
             rf"knn_tile_topk_kernel<{wr}, {wq}, \d+, \d+, \d+, {path}, \d+>")
 
 
+def pmc_record(pattern: str, suffix: str):
+    """The record of the newest profiles/*<suffix> (by round/version in the name) whose kernel
+    name matches `pattern`, or None."""
+    import glob
+    import re
+    pat = re.compile(pattern)
+
+    def version(f):
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*" + suffix)), key=version, reverse=True):
+        try:
+            data = json.load(open(f))
+        except Exception:
+            continue
+        for name, rec in data.items():
+            if pat.search(name):
+                return rec, os.path.basename(f)
+    return None
+
+
 def pmc_traffic(pattern: str):
     """HBM bytes per launch of the fused kernel from the newest profiles/*_traffic.json written by
     tools/pmc_traffic.sh (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected), or None."""
@@ -312,6 +333,7 @@ def main():
     if world > 1:
         dist.all_reduce(e1, op=dist.ReduceOp.MAX)
     el1, kern1_ms = float(e1[0]), float(e1[1])
+    path1 = lib.knn_last_path(shard.index.handle)          # 0 exact, 1 split, 2 bf16
 
     tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
     lib.knn_plan(shard.index.handle, a.nq, a.k, C.byref(tr), C.byref(tq), C.byref(sp), C.byref(wg))
@@ -336,7 +358,12 @@ def main():
                           path, "fp32 dense MFMA (v_mfma_f32_32x32x2_f32)")
         dtype = {2: "bf16 candidates (fp32 accumulate) + fp32 rerank, certified exact",
                  1: "bf16x3 split (fp32-equivalent) + fp32 rerank"}.get(path, "fp32")
-        bytes1 = 4.0 * n_local * D_total + 4.0 * n_local
+        bytes1 = 4.0 * n_local * D_total + 4.0 * n_local    # the fp32 corpus + norms (algorithmic)
+        dpb = (D_total + 63) // 64 * 64
+        # what the single-query kernel actually streams: the bf16 copy (bf16 path), the split copy
+        # (hi + lo, as much as fp32) or the fp32 rows
+        stream1 = (2.0 * n_local * dpb if path1 == 2 else 4.0 * n_local * D_total) + 4.0 * n_local
+        busy = pmc_record(kpat, "_clock.json") if world == 1 else None
         qps = a.nq * a.steps / elapsed
         out = {
             "metric": "k-NN queries/sec + recall@10 on 1M concat vectors at 1/2/4/8 MI355X",
@@ -373,13 +400,18 @@ def main():
                 "traffic_source": traffic[1] if traffic else None,
                 "kernel": kname,
                 "kernel_ms": kern_ms,
+                "mfma_busy": busy[0]["mfma_busy"] if busy else None,
+                "clock_ghz": busy[0]["clock_ghz"] if busy else None,
+                "busy_source": busy[1] if busy else None,
                 "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
             },
             "single_query": {
                 "queries_per_s": a.single_query_steps / el1,
                 "kernel_ms": kern1_ms,
-                "hbm_gbs": bytes1 / (kern1_ms * 1e-3) / 1e9,
-                "hbm_frac": bytes1 / (kern1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "path": {0: "exact", 1: "split", 2: "bf16"}.get(path1, "?"),
+                "hbm_gbs": stream1 / (kern1_ms * 1e-3) / 1e9,
+                "hbm_frac": stream1 / (kern1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "fp32_equivalent_gbs": bytes1 / (kern1_ms * 1e-3) / 1e9,
             },
             "build_s": build_s,
             "cpu_baseline": cpu,

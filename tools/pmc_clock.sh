@@ -22,5 +22,10 @@ clk = g / 8 / t
 m = sum(agg["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(agg["SQ_VALU_MFMA_BUSY_CYCLES"])
 print(f"{d.split('/')[-1]:24s} dur {t*1e3:.3f} ms  clock {clk/1e9:.2f} GHz  MFMA busy {m / (256*4*clk*t):.1%}  "
       f"MFMA insts {sum(agg['SQ_INSTS_MFMA'])/len(agg['SQ_INSTS_MFMA']):.4g}")
+import json, os
+kern = next(csv.DictReader(open(f[0])))["Kernel_Name"].split("(")[0]
+json.dump({kern: {"clock_ghz": clk / 1e9, "mfma_busy": m / (256 * 4 * clk * t), "dur_ms_under_pmc": t * 1e3,
+                  "note": "clock = GRBM_GUI_ACTIVE / 8 XCDs / duration; busy = SQ_VALU_MFMA_BUSY_CYCLES / (256 CUs x 4 SIMDs x cycles)"}},
+          open(os.path.join(os.path.dirname(d), os.path.basename(d) + "_clock.json"), "w"), indent=1)
 PY
 done
