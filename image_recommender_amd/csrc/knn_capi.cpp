@@ -160,6 +160,10 @@ inline float b16_acc_coef(int dpb) {
 // kernel (the merge floor covers what a lane list drops).
 constexpr int kB16Cand = 64;
 inline int b16_km(int k) { return k <= 16 ? 16 : 32; }
+#ifndef IMGREC_B16_NARROW_Q
+#define IMGREC_B16_NARROW_Q 32
+#endif
+constexpr int kB16NarrowQ = IMGREC_B16_NARROW_Q;   // batches up to this use the 32-query tile
 
 // bf16-path geometry: large batches with k <= 10 on the 256 x 256-tile kernel (one workgroup
 // per CU, lane lists of 8 / 10); otherwise (kB16WR, kB16WQ) workgroups, kB16WGPCU per CU.
@@ -182,8 +186,11 @@ Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus, int dpb) {
         return p;
     }
     p.km = b16_km(k);
-    p.wr = imgrec::kB16WR;
-    p.wq = imgrec::kB16WQ;
+    // batches of <= 32 queries: a 32-query tile (the (1,4) tile would pad them to 128 and spend
+    // four times the matrix work of an HBM-bound search)
+    const bool narrow = nq <= kB16NarrowQ;
+    p.wr = narrow ? 2 : imgrec::kB16WR;
+    p.wq = narrow ? 1 : imgrec::kB16WQ;
     p.bm = p.wr * 32 * imgrec::kB16WB;
     p.bq = p.wq * 32;
     p.nqb = (int)((nq + p.bq - 1) / p.bq);

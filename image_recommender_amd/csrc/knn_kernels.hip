@@ -682,8 +682,12 @@ hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
     if (a.mode == kModeBF16) {
         // bf16 candidate pass: rows of dp bf16 = dp/2 words, 64-deep (32-word) stages
         if (a.dp % 32 != 0 || (a.km != 16 && a.km != 32)) return hipErrorInvalidValue;
-        if (a.wb != kB16WB || a.wr != kB16WR || a.wq != kB16WQ) return hipErrorInvalidValue;
-        return launch_tile_km<kB16WR, kB16WQ, kB16NS, 32, kModeBF16, kB16WB>(a.km, a, st);
+        if (a.wb != kB16WB) return hipErrorInvalidValue;
+        if (a.wr == kB16WR && a.wq == kB16WQ)
+            return launch_tile_km<kB16WR, kB16WQ, kB16NS, 32, kModeBF16, kB16WB>(a.km, a, st);
+        // small batches: 256 rows x 32 queries, two 2-wave workgroups per CU
+        if (a.wr == 2 && a.wq == 1) return launch_tile_km<2, 1, 2, 32, kModeBF16, kB16WB>(a.km, a, st);
+        return hipErrorInvalidValue;
     }
     if (a.mode == kModeSplit) {
         // split-bf16 candidate pass (knn_refine.hip certifies and reranks its output); the
