@@ -45,6 +45,9 @@ SIGNATURES = {
     "knn_merge_device": (_i, [_vp, _vp, _i, _i64, _i, _i, _i, _vp, _vp, _vp]),
     "knn_packed_bytes": (_i64, [_i64, _i]),
     "knn_merge_packed_device": (_i, [_vp, _i, _i64, _i, _i, _i, _vp, _vp, _vp]),
+    # imgrec_ivfpq.h
+    "ivfpq_lut_device": (_i, [_vp, _i64, _i, _i, _i, _vp, _vp, _vp]),
+    "ivfpq_scan_device": (_i, [_vp, _vp, _i64, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "knn_write": (_i, [_vp, C.c_char_p]),
     "knn_read": (_i, [C.c_char_p, _i, C.POINTER(_vp)]),
     "knn_normalize_L2": (_i, [_vp, _i64, _i]),

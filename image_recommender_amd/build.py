@@ -28,8 +28,9 @@ LIB = LIBDIR / os.environ.get("IMGREC_LIB_NAME", "libimgrec.so")
 EXTRA_FLAGS = os.environ.get("IMGREC_EXTRA_FLAGS", "").split()
 ARCH = os.environ.get("IMGREC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_refine.hip", "knn_capi.cpp", "color_hist.hip", "ingest.cpp"]
-HEADERS = ["knn_kernels.h", "../../include/imgrec_knn.h", "../../include/imgrec_color.h",
+SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_refine.hip", "knn_capi.cpp", "color_hist.hip", "ingest.cpp",
+           "ivfpq.hip"]
+HEADERS = ["knn_kernels.h", "wave_ops.h", "../../include/imgrec_ivfpq.h", "../../include/imgrec_knn.h", "../../include/imgrec_color.h",
            "../../include/imgrec_ingest.h"]
 
 

@@ -1,0 +1,147 @@
+// ivfpq.hip — GPU IVF-PQ search kernels (gfx950): per-query distance tables and the ADC list scan.
+//
+// The reference's default index is faiss IndexIVFPQ(IndexHNSWFlat(d, 32), d, 2048, m, 12) with
+// nprobe 1 (/root/reference/main/create_index.py:218-228; searched at
+// main/search_from_image.py:247).  These kernels restate faiss's search arithmetic for it
+// (by-residual L2 product quantisation, distance-table ADC; oracle/ivfpq.py is the CPU
+// statement the tests hold them to):
+//
+//   ivfpq_lut_kernel   one workgroup per (residual, sub-quantiser): the residual sub-vector sits
+//                      in LDS, each thread scores centroids i, i + 256, ... of the transposed
+//                      codebook (coalesced columns): lut[r][j][i] = sum_t (r_jt - c_jit)^2.
+//   ivfpq_scan_kernel  one wave per query: lanes take the rows of the probed lists round-robin,
+//                      a row's distance is the sum over j of lut[j][code_j] (fp32, j ascending),
+//                      kept in a per-lane (distance, label) list; the k results are k rounds of a
+//                      wave-wide u64 minimum over the lane heads (order-preserving key bits |
+//                      label), the winning lane popping its head.
+//
+// Both are memory-light next to the exact path: the scan reads m codes (2 B each) and m table
+// entries per row of the probed lists (~N / nlist rows per probe).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <float.h>
+#include <math.h>
+
+#include "knn_kernels.h"
+#include "wave_ops.h"
+
+namespace imgrec {
+namespace {
+
+constexpr int kLutThreads = 256;
+constexpr int kMaxDsub = 256;
+
+__global__ void __launch_bounds__(kLutThreads)
+ivfpq_lut_kernel(const float* __restrict__ resid, int d, int m, int ksub,
+                 const float* __restrict__ cbt, float* __restrict__ lut) {
+    __shared__ float sr[kMaxDsub];
+    const int64_t r = blockIdx.x;
+    const int j = blockIdx.y;
+    const int dsub = d / m;
+    for (int t = threadIdx.x; t < dsub; t += kLutThreads) sr[t] = resid[r * d + (int64_t)j * dsub + t];
+    __syncthreads();
+    const float* cb = cbt + (size_t)j * dsub * ksub;
+    float* out = lut + ((size_t)r * m + j) * ksub;
+    for (int i = threadIdx.x; i < ksub; i += kLutThreads) {
+        float acc = 0.f;
+        for (int t = 0; t < dsub; ++t) {
+            const float df = sr[t] - cb[(size_t)t * ksub + i];
+            acc = fmaf(df, df, acc);
+        }
+        out[i] = acc;
+    }
+}
+
+// (d1, i1) before (d2, i2): smaller distance, ties by smaller label; label -1 = empty, last.
+__device__ __forceinline__ bool before(float d1, int i1, float d2, int i2) {
+    return i2 < 0 || d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+template <int KM>
+__device__ __forceinline__ void insert_sorted(float (&kd)[KM], int (&ki)[KM], float d, int id) {
+#pragma unroll
+    for (int p = KM - 1; p > 0; --p) {
+        const bool shift = before(d, id, kd[p - 1], ki[p - 1]);
+        const bool here = !shift && before(d, id, kd[p], ki[p]);
+        kd[p] = shift ? kd[p - 1] : (here ? d : kd[p]);
+        ki[p] = shift ? ki[p - 1] : (here ? id : ki[p]);
+    }
+    const bool here0 = before(d, id, kd[0], ki[0]);
+    kd[0] = here0 ? d : kd[0];
+    ki[0] = here0 ? id : ki[0];
+}
+
+template <int KM>
+__global__ void __launch_bounds__(256)
+ivfpq_scan_kernel(const float* __restrict__ lut, const int64_t* __restrict__ probes, int64_t nq,
+                  int nprobe, const int64_t* __restrict__ list_off,
+                  const uint16_t* __restrict__ codes, const int64_t* __restrict__ ids, int m,
+                  int ksub, int k, float* __restrict__ D, int64_t* __restrict__ I) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;                                        // whole wave
+    float kd[KM];
+    int ki[KM];
+#pragma unroll
+    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+    for (int p = 0; p < nprobe; ++p) {
+        const int64_t l = probes[q * nprobe + p];
+        if (l < 0) continue;
+        const float* T = lut + (size_t)(q * nprobe + p) * m * ksub;
+        const int64_t r1 = list_off[l + 1];
+        for (int64_t row = list_off[l] + lane; row < r1; row += 64) {
+            const uint16_t* c = codes + row * m;
+            float dist = 0.f;
+            for (int j = 0; j < m; ++j) dist += T[(size_t)j * ksub + c[j]];
+            const int id = (int)ids[row];
+            if (before(dist, id, kd[KM - 1], ki[KM - 1])) insert_sorted<KM>(kd, ki, dist, id);
+        }
+    }
+    // k rounds of the wave minimum over the lane heads
+    constexpr uint64_t kEmpty = ~0ull;
+    for (int r = 0; r < k; ++r) {
+        const uint64_t v = ki[0] < 0 ? kEmpty : ((uint64_t)key_bits_ordered(kd[0]) << 32) | (uint32_t)ki[0];
+        const uint64_t b = wave_min_u64(v);
+        if (b != kEmpty && v == b) {
+#pragma unroll
+            for (int p = 0; p < KM - 1; ++p) { kd[p] = kd[p + 1]; ki[p] = ki[p + 1]; }
+            kd[KM - 1] = INFINITY;
+            ki[KM - 1] = -1;
+        }
+        if (lane == 0) {
+            D[q * k + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
+            I[q * k + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_ivfpq_lut(const float* resid, int64_t nr, int d, int m, int ksub,
+                            const float* cbt, float* lut, hipStream_t st) {
+    if (nr <= 0) return hipSuccess;
+    if (m <= 0 || d % m != 0 || d / m > kMaxDsub || ksub <= 0 || nr > 0x7fffffff || m > 65535)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ivfpq_lut_kernel, dim3((unsigned)nr, (unsigned)m), dim3(kLutThreads), 0, st,
+                       resid, d, m, ksub, cbt, lut);
+    return hipGetLastError();
+}
+
+hipError_t launch_ivfpq_scan(const float* lut, const int64_t* probes, int64_t nq, int nprobe,
+                             const int64_t* list_off, const uint16_t* codes, const int64_t* ids,
+                             int m, int ksub, int k, float* D, int64_t* I, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (k <= 0 || k > 32 || nprobe <= 0 || m <= 0 || ksub <= 0 || ksub > 65536)
+        return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
+    if (k <= 16)
+        hipLaunchKernelGGL((ivfpq_scan_kernel<16>), grid, block, 0, st, lut, probes, nq, nprobe,
+                           list_off, codes, ids, m, ksub, k, D, I);
+    else
+        hipLaunchKernelGGL((ivfpq_scan_kernel<32>), grid, block, 0, st, lut, probes, nq, nprobe,
+                           list_off, codes, ids, m, ksub, k, D, I);
+    return hipGetLastError();
+}
+
+}  // namespace imgrec

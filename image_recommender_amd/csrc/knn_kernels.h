@@ -142,4 +142,11 @@ hipError_t launch_query_prep_b16(const float* src, int64_t n, int d, int dp, int
                                  hipStream_t st);
 hipError_t launch_max_norm(const float* xn, int64_t n, float* out, hipStream_t st);
 
+// IVF-PQ (ivfpq.hip; layouts in include/imgrec_ivfpq.h)
+hipError_t launch_ivfpq_lut(const float* resid, int64_t nr, int d, int m, int ksub,
+                            const float* cbt, float* lut, hipStream_t st);
+hipError_t launch_ivfpq_scan(const float* lut, const int64_t* probes, int64_t nq, int nprobe,
+                             const int64_t* list_off, const uint16_t* codes, const int64_t* ids,
+                             int m, int ksub, int k, float* D, int64_t* I, hipStream_t st);
+
 }  // namespace imgrec
