@@ -85,14 +85,21 @@ class IndexIVFPQ:
             raise ValueError("expected a 2-D array")
         return t.contiguous()
 
-    def _nearest(self, x, c, k: int = 1):
-        """(n, k) int64 indices of the k nearest rows of c (exact fp32 k-NN kernels)."""
+    def _flat(self, c):
+        """Exact fp32 k-NN index over the rows of c."""
         torch = _torch()
         idx = IndexFlatL2(c.shape[1], device=self.device.index)
         idx.search_mode = "exact"
         c = c.contiguous()
+        idx.add_device(c.data_ptr(), c.shape[0], torch.cuda.current_stream(self.device).cuda_stream)
+        return idx
+
+    def _nearest(self, x, c, k: int = 1, idx=None):
+        """(n, k) int64 indices of the k nearest rows of c (exact fp32 k-NN kernels)."""
+        torch = _torch()
+        temp = idx is None
+        idx = self._flat(c) if temp else idx
         st = torch.cuda.current_stream(self.device).cuda_stream
-        idx.add_device(c.data_ptr(), c.shape[0], st)
         n = x.shape[0]
         D = torch.empty((n, k), dtype=torch.float32, device=self.device)
         I = torch.empty((n, k), dtype=torch.int64, device=self.device)
@@ -100,7 +107,8 @@ class IndexIVFPQ:
             r1 = min(n, r0 + (1 << 20))
             xs = x[r0:r1].contiguous()
             idx.search_device(xs.data_ptr(), r1 - r0, k, D[r0:r1].data_ptr(), I[r0:r1].data_ptr(), st)
-        torch.cuda.synchronize(self.device)
+        if temp:        # the temporary index's memory must outlive the enqueued search
+            torch.cuda.synchronize(self.device)
         return I
 
     def _kmeans(self, x, k: int, niter: int, seed: int):
@@ -154,6 +162,7 @@ class IndexIVFPQ:
 
     def _set(self, cen, cb) -> None:
         self.centroids = cen.contiguous()
+        self._coarse = self._flat(self.centroids)       # the coarse quantiser, kept resident
         self.codebooks = cb.contiguous()
         self._cbt = cb.permute(0, 2, 1).contiguous()
         self.is_trained = True
@@ -162,7 +171,7 @@ class IndexIVFPQ:
         """(list id (n,), codes (n, m) int64) of the rows of x."""
         torch = _torch()
         x = self._tensor(x)
-        lists = self._nearest(x, self.centroids)[:, 0]
+        lists = self._nearest(x, self.centroids, 1, self._coarse)[:, 0]
         r = x - self.centroids[lists]
         codes = torch.empty((x.shape[0], self.m), dtype=torch.int64, device=self.device)
         for j in range(self.m):
@@ -226,7 +235,7 @@ class IndexIVFPQ:
         for q0 in range(0, nq, chunk):
             q1 = min(nq, q0 + chunk)
             qc = q[q0:q1]
-            probes = self._nearest(qc, self.centroids, npb).contiguous()
+            probes = self._nearest(qc, self.centroids, npb, self._coarse).contiguous()
             resid = (qc[:, None, :] - self.centroids[probes]).reshape(-1, self.d).contiguous()
             lut = torch.empty((resid.shape[0], self.m, self.ksub), dtype=torch.float32, device=self.device)
             _lib.check(lib.ivfpq_lut_device(C.c_void_p(resid.data_ptr()), resid.shape[0], self.d,
