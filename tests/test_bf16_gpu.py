@@ -205,6 +205,8 @@ def test_bf16_mode_rejected_for_tiny_d(faiss):
     (777, 256, 513, 1, "l2"),         # tiny corpus: partial last tile, splits of one tile
     (30000, 768, 1024, 10, "cosine"),
     (40000, 512, 1024, 5, "l2"),
+    (5, 64, 600, 10, "l2"),           # fewer rows than k: one 8-row group, padded results
+    (2061, 128, 777, 9, "ip"),        # ragged last group (2061 = 257 x 8 + 5), partial tiles
 ])
 def test_bf16_big_tile_kernel(faiss, n, d, nq, k, metric):
     """Batches of >= 512 queries with k <= 10 run the 256 x 256-tile kernel (knn_b16.hip)."""
