@@ -1,0 +1,77 @@
+"""ShardedIndex.search end to end on the GPU: two ranks (gloo, both on cuda:0 — the 8-GPU RCCL run
+belongs to the driver) each hold a row shard, search into their packed chunk, gather it in one
+collective and merge with knn_merge_packed_device; the result equals one index over all rows
+(SURVEY.md §8e)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def faiss(gpu):
+    from image_recommender_amd import faiss_compat
+    return faiss_compat
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, d, nq, k, mode, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from image_recommender_amd.faiss_compat import METRIC_L2
+        from image_recommender_amd.sharded import ShardedIndex
+        from tests.datagen import mixture
+        torch.cuda.set_device(0)
+        xb = mixture(n, d, centres=40, seed=31)
+        xq = torch.from_numpy(mixture(nq, d, centres=40, seed=32)).cuda()
+        sh = ShardedIndex(d, n, METRIC_L2, device=0)
+        sh.add_local(xb[sh.row0:sh.row1])
+        sh.index.search_mode = mode
+        for _ in range(2):                                  # second call: cached chunk buffers
+            D, I = sh.search(xq, k)
+        torch.cuda.synchronize()
+        if rank == 0:
+            out.put((D.cpu().numpy(), I.cpu().numpy(), sh.index.search_stats()[1]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,d,nq,k,mode", [(20000, 96, 64, 10, "exact"), (30000, 256, 600, 10, "bf16"),
+                                           (4001, 64, 7, 5, "exact")])
+def test_sharded_search_two_ranks_equals_one_index(faiss, n, d, nq, k, mode):
+    import torch.multiprocessing as mp
+    from tests.datagen import mixture
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, d, nq, k, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    D, I, fallbacks = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    xb, xq = mixture(n, d, centres=40, seed=31), mixture(nq, d, centres=40, seed=32)
+    full = faiss.IndexFlatL2(d)
+    full.add(xb)
+    full.search_mode = mode
+    Df, If = full.search(xq, k)
+    if fallbacks or full.search_stats()[1]:
+        assert (I == If).mean() > 0.99
+        return
+    np.testing.assert_array_equal(I, If)
+    np.testing.assert_array_equal(D, Df)
