@@ -252,6 +252,28 @@ class IndexIVFPQ:
         torch.cuda.synchronize(self.device)
         return D.cpu().numpy(), I.cpu().numpy()
 
+    # ---- persistence ----------------------------------------------------------------------------
+    def write(self, path) -> None:
+        """Save to an .npz file (plain arrays; read back with ``IndexIVFPQ.read``).  faiss's own
+        IVF-PQ file layout is not reproduced (it would need faiss to verify)."""
+        if not self.is_trained:
+            raise RuntimeError("write: index is not trained")
+        lists, codes, ids = self.list_contents()
+        with open(path, "wb") as f:
+            np.savez(f, header=np.array([self.d, self.nlist, self.m, self.nbits, self.nprobe], np.int64),
+                     centroids=self.centroids.cpu().numpy(), codebooks=self.codebooks.cpu().numpy(),
+                     lists=lists, codes=codes.astype(np.uint16), ids=ids)
+
+    @classmethod
+    def read(cls, path, device: int = 0) -> "IndexIVFPQ":
+        with np.load(path, allow_pickle=False) as z:
+            d, nlist, m, nbits, nprobe = (int(v) for v in z["header"])
+            idx = cls(d, nlist, m, nbits, device=device)
+            idx.set_trained(z["centroids"], z["codebooks"])
+            idx.add_encoded(z["lists"], z["codes"].astype(np.int64), z["ids"])
+        idx.nprobe = nprobe
+        return idx
+
     # ---- introspection (tests) ----------------------------------------------------------------
     def list_contents(self):
         """(list id, codes (n, m) int64, labels) of the stored rows, in storage order (numpy)."""

@@ -123,3 +123,19 @@ def test_rejects_bad_shapes(gpu):
         idx.add_encoded([0], [[0, 0, 0, 16]], [0])
     with pytest.raises(NotImplementedError):
         idx.search(np.zeros((1, 16), np.float32), 33)
+
+
+def test_write_read_roundtrip(gpu, tmp_path):
+    from image_recommender_amd.ivfpq import IndexIVFPQ
+    rng = np.random.default_rng(12)
+    idx, cen, cb, lists, codes, ids = _random_index(IndexIVFPQ, rng, 32, 8, 4, 10, 2000)
+    idx.nprobe = 3
+    q = rng.standard_normal((9, 32)).astype(np.float32)
+    D0, I0 = idx.search(q, 7)
+    f = tmp_path / "ivfpq.npz"
+    idx.write(f)
+    back = IndexIVFPQ.read(f)
+    assert back.ntotal == idx.ntotal and back.nprobe == 3 and back.nbits == 10
+    D1, I1 = back.search(q, 7)
+    np.testing.assert_array_equal(I1, I0)
+    np.testing.assert_array_equal(D1, D0)
