@@ -6,14 +6,16 @@
 // (by-residual L2 product quantisation, distance-table ADC; oracle/ivfpq.py is the CPU
 // statement the tests hold them to):
 //
-//   ivfpq_lut_kernel   one workgroup per (residual, sub-quantiser): the residual sub-vector sits
-//                      in LDS, each thread scores centroids i, i + 256, ... of the transposed
-//                      codebook (coalesced columns): lut[r][j][i] = sum_t (r_jt - c_jit)^2.
-//   ivfpq_scan_kernel  one wave per query: lanes take the rows of the probed lists round-robin,
-//                      a row's distance is the sum over j of lut[j][code_j] (fp32, j ascending),
-//                      kept in a per-lane (distance, label) list; the k results are k rounds of a
-//                      wave-wide u64 minimum over the lane heads (order-preserving key bits |
-//                      label), the winning lane popping its head.
+//   ivfpq_lut_kernel   one workgroup per (8 residuals, sub-quantiser): the residual sub-vectors
+//                      sit in LDS, each thread scores centroids i, i + 256, ... of the transposed
+//                      codebook (coalesced columns, each read serving 8 residuals):
+//                      lut[r][j][i] = sum_t (r_jt - c_jit)^2.
+//   ivfpq_scan_kernel  one 4-wave workgroup per query: its 256 lanes take the rows of the probed
+//                      lists round-robin, a row's distance is the sum over j of lut[j][code_j]
+//                      (fp32, j ascending), kept in a per-lane (distance, label) list; each wave
+//                      reduces its lanes to k by k rounds of a wave-wide u64 minimum over the lane
+//                      heads (order-preserving key bits | label), then the first wave merges the
+//                      four lists the same way.
 //
 // Both are memory-light next to the exact path: the scan reads m codes (2 B each) and m table
 // entries per row of the probed lists (~N / nlist rows per probe).
@@ -32,24 +34,37 @@ namespace {
 constexpr int kLutThreads = 256;
 constexpr int kMaxDsub = 256;
 
+constexpr int kLutRes = 8;          // residuals per workgroup: each codebook column read serves 8
+
 __global__ void __launch_bounds__(kLutThreads)
-ivfpq_lut_kernel(const float* __restrict__ resid, int d, int m, int ksub,
+ivfpq_lut_kernel(const float* __restrict__ resid, int64_t nr, int d, int m, int ksub,
                  const float* __restrict__ cbt, float* __restrict__ lut) {
-    __shared__ float sr[kMaxDsub];
-    const int64_t r = blockIdx.x;
+    __shared__ float sr[kLutRes][kMaxDsub];
+    const int64_t r0 = (int64_t)blockIdx.x * kLutRes;
     const int j = blockIdx.y;
     const int dsub = d / m;
-    for (int t = threadIdx.x; t < dsub; t += kLutThreads) sr[t] = resid[r * d + (int64_t)j * dsub + t];
+    const int nres = (int)min((int64_t)kLutRes, nr - r0);
+    for (int e = threadIdx.x; e < kLutRes * dsub; e += kLutThreads) {
+        const int r = e / dsub, t = e - r * dsub;
+        sr[r][t] = r < nres ? resid[(r0 + r) * d + (int64_t)j * dsub + t] : 0.f;
+    }
     __syncthreads();
     const float* cb = cbt + (size_t)j * dsub * ksub;
-    float* out = lut + ((size_t)r * m + j) * ksub;
     for (int i = threadIdx.x; i < ksub; i += kLutThreads) {
-        float acc = 0.f;
+        float acc[kLutRes];
+#pragma unroll
+        for (int r = 0; r < kLutRes; ++r) acc[r] = 0.f;
         for (int t = 0; t < dsub; ++t) {
-            const float df = sr[t] - cb[(size_t)t * ksub + i];
-            acc = fmaf(df, df, acc);
+            const float c = cb[(size_t)t * ksub + i];
+#pragma unroll
+            for (int r = 0; r < kLutRes; ++r) {
+                const float df = sr[r][t] - c;
+                acc[r] = fmaf(df, df, acc[r]);
+            }
         }
-        out[i] = acc;
+#pragma unroll
+        for (int r = 0; r < kLutRes; ++r)
+            if (r < nres) lut[((size_t)(r0 + r) * m + j) * ksub + i] = acc[r];
     }
 }
 
@@ -78,9 +93,10 @@ ivfpq_scan_kernel(const float* __restrict__ lut, const int64_t* __restrict__ pro
                   int nprobe, const int64_t* __restrict__ list_off,
                   const uint16_t* __restrict__ codes, const int64_t* __restrict__ ids, int m,
                   int ksub, int k, float* __restrict__ D, int64_t* __restrict__ I) {
-    const int lane = threadIdx.x & 63;
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;                                        // whole wave
+    // one 4-wave workgroup per query: the probed rows go round-robin over its 256 lanes
+    __shared__ uint64_t best[4][32];                            // each wave's k best, ascending
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t q = blockIdx.x;
     float kd[KM];
     int ki[KM];
 #pragma unroll
@@ -90,7 +106,7 @@ ivfpq_scan_kernel(const float* __restrict__ lut, const int64_t* __restrict__ pro
         if (l < 0) continue;
         const float* T = lut + (size_t)(q * nprobe + p) * m * ksub;
         const int64_t r1 = list_off[l + 1];
-        for (int64_t row = list_off[l] + lane; row < r1; row += 64) {
+        for (int64_t row = list_off[l] + threadIdx.x; row < r1; row += 256) {
             const uint16_t* c = codes + row * m;
             float dist = 0.f;
             for (int j = 0; j < m; ++j) dist += T[(size_t)j * ksub + c[j]];
@@ -98,7 +114,7 @@ ivfpq_scan_kernel(const float* __restrict__ lut, const int64_t* __restrict__ pro
             if (before(dist, id, kd[KM - 1], ki[KM - 1])) insert_sorted<KM>(kd, ki, dist, id);
         }
     }
-    // k rounds of the wave minimum over the lane heads
+    // per wave: k rounds of the wave minimum over the lane heads
     constexpr uint64_t kEmpty = ~0ull;
     for (int r = 0; r < k; ++r) {
         const uint64_t v = ki[0] < 0 ? kEmpty : ((uint64_t)key_bits_ordered(kd[0]) << 32) | (uint32_t)ki[0];
@@ -109,6 +125,16 @@ ivfpq_scan_kernel(const float* __restrict__ lut, const int64_t* __restrict__ pro
             kd[KM - 1] = INFINITY;
             ki[KM - 1] = -1;
         }
+        if (lane == 0) best[wave][r] = b;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    // the four waves' sorted lists: lane w < 4 holds the head of list w
+    int head = 0;
+    uint64_t cur = lane < 4 ? best[lane][0] : kEmpty;
+    for (int r = 0; r < k; ++r) {
+        const uint64_t b = wave_min_u64(cur);
+        if (b != kEmpty && cur == b) cur = ++head < k ? best[lane][head] : kEmpty;
         if (lane == 0) {
             D[q * k + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
             I[q * k + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b;
@@ -123,8 +149,8 @@ hipError_t launch_ivfpq_lut(const float* resid, int64_t nr, int d, int m, int ks
     if (nr <= 0) return hipSuccess;
     if (m <= 0 || d % m != 0 || d / m > kMaxDsub || ksub <= 0 || nr > 0x7fffffff || m > 65535)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(ivfpq_lut_kernel, dim3((unsigned)nr, (unsigned)m), dim3(kLutThreads), 0, st,
-                       resid, d, m, ksub, cbt, lut);
+    hipLaunchKernelGGL(ivfpq_lut_kernel, dim3((unsigned)((nr + kLutRes - 1) / kLutRes), (unsigned)m),
+                       dim3(kLutThreads), 0, st, resid, nr, d, m, ksub, cbt, lut);
     return hipGetLastError();
 }
 
@@ -134,7 +160,7 @@ hipError_t launch_ivfpq_scan(const float* lut, const int64_t* probes, int64_t nq
     if (nq <= 0) return hipSuccess;
     if (k <= 0 || k > 32 || nprobe <= 0 || m <= 0 || ksub <= 0 || ksub > 65536)
         return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((nq + 3) / 4)), block(256);
+    const dim3 grid((unsigned)nq), block(256);
     if (k <= 16)
         hipLaunchKernelGGL((ivfpq_scan_kernel<16>), grid, block, 0, st, lut, probes, nq, nprobe,
                            list_off, codes, ids, m, ksub, k, D, I);

@@ -231,7 +231,7 @@ class IndexIVFPQ:
             return D.cpu().numpy(), I.cpu().numpy()
         lib = _lib.load()
         st = torch.cuda.current_stream(self.device).cuda_stream
-        chunk = max(1, (1 << 28) // (npb * self.m * self.ksub * 4))     # <= 256 MB of tables
+        chunk = max(1, (1 << 30) // (npb * self.m * self.ksub * 4))     # <= 1 GB of tables
         for q0 in range(0, nq, chunk):
             q1 = min(nq, q0 + chunk)
             qc = q[q0:q1]
