@@ -406,25 +406,38 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
-        float cth[2];
+        // the other row-half wave's published J-th bounds (read once per tile)
+        float other[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const float tau = kd[h][KM - 1];
-            const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
 #ifdef IMGREC_ABLATE_NO_SHARE
-            const float other = INFINITY;
+            other[h] = INFINITY;
 #else
-            const float other = share[(((1 - wr) * 4 + wq) * 2 + h) * 32 + li];
+            other[h] = share[(((1 - wr) * 4 + wq) * 2 + h) * 32 + li];
 #endif
-            const float T = fminf(fminf(tau, __shfl_xor(tau, 32, 64)), fmaxf(jb, other));
-            const float c = L2 ? 0.5f * (qn[h] - T) - kLo * (qn[h] + fabsf(T)) : -T;
-            cth[h] = qcol[h] < nq ? c : INFINITY;
         }
+        float cth[2];
+        auto screen = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float tau = kd[h][KM - 1];
+                const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
+                const float T = fminf(fminf(tau, __shfl_xor(tau, 32, 64)), fmaxf(jb, other[h]));
+                const float c = L2 ? 0.5f * (qn[h] - T) - kLo * (qn[h] + fabsf(T)) : -T;
+                cth[h] = qcol[h] < nq ? c : INFINITY;
+            }
+        };
+        screen();
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
 #ifdef IMGREC_ABLATE_NO_EPILOGUE
             asm volatile("" ::"v"(acc[rb][0]), "v"(acc[rb][1]));
             continue;
+#endif
+#ifndef IMGREC_B16_SCREEN_ONCE
+            // re-tighten after the previous block's insertions (in the first tile the empty lists
+            // would otherwise pass every row of all four blocks)
+            if (rb > 0) screen();
 #endif
             const int rbase = wr * 128 + rb * 32 + 4 * lh;      // tile row of accumulator reg 0
             unsigned live = 0xffffu;                            // rows of the block that count
