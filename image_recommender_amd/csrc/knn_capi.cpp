@@ -233,9 +233,12 @@ struct knn_index {
     uint32_t* qsplit = nullptr; size_t qsplit_cap = 0;
     float* cand2_d = nullptr; size_t cand2_d_cap = 0;
     int64_t* cand2_i = nullptr; size_t cand2_i_cap = 0;
-    // [0] = uncertified count, [1] = max observed error / bound (float bits), [2..] = their list
+    // [0] = uncertified count, [1] = max observed error / bound (float bits), [2] unused,
+    // [3..] = the uncertified queries; [0..1] are zero between searches
     int* fail = nullptr; size_t fail_cap = 0;
-    int* hstat = nullptr;                               // pinned host copy of fail[0..1]
+    int* mail = nullptr;                                // pinned, mapped: [seq, count, ratio bits]
+    int* mail_dev = nullptr;                            // its device address
+    int mail_seq = 0;
     float last_err_ratio = 0.f;
     uint16_t* qb16 = nullptr; size_t qb16_cap = 0;
     float* q_resid = nullptr; size_t q_resid_cap = 0;
@@ -415,13 +418,53 @@ bool use_split(const knn_index* ix, int64_t nq, int k) {
 int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
                 int64_t* I, hipStream_t st, bool timed);
 
-// Uncertified count and max error ratio of the last rerank: one 8-byte copy into pinned memory.
+// Workspace for the rerank's stats: counters zeroed once here (the publish kernel after every
+// rerank zeroes them again) and the pinned host mailbox it publishes to.
+int grow_fail(knn_index* ix, int64_t nq, hipStream_t st) {
+    if (!ix->mail) {
+        KNN_HIP(hipHostMalloc((void**)&ix->mail, 4 * sizeof(int),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(ix->mail, 0, 4 * sizeof(int));
+        KNN_HIP(hipHostGetDevicePointer((void**)&ix->mail_dev, ix->mail, 0));
+    }
+    if (ix->fail_cap >= (size_t)nq + 3) return KNN_OK;
+    int rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 3);
+    if (rc != KNN_OK) return rc;
+    KNN_HIP(hipMemsetAsync(ix->fail, 0, 3 * sizeof(int), st));
+    return KNN_OK;
+}
+
+// Point a rerank at the stats workspace; the next mailbox sequence number goes with it.
+void bind_stats(knn_index* ix, imgrec::RerankArgs* r) {
+    r->fail_count = ix->fail;
+    r->err_ratio = reinterpret_cast<float*>(ix->fail + 1);
+    r->fail_list = ix->fail + 3;
+    r->mail = ix->mail_dev;
+    r->seq = ++ix->mail_seq;
+    if (r->seq <= 0) r->seq = ix->mail_seq = 1;          // 0 is the mailbox's initial value
+}
+
+// Uncertified count and max error ratio of the last rerank: spin on the host mailbox the publish
+// kernel writes (no copy, no stream synchronisation), with a stream query now and then so
+// that a failed or drained stream ends the wait.
 int read_stats(knn_index* ix, hipStream_t st, int* nfail, float* ratio) {
-    if (!ix->hstat) KNN_HIP(hipHostMalloc((void**)&ix->hstat, 2 * sizeof(int), hipHostMallocDefault));
-    KNN_HIP(hipMemcpyAsync(ix->hstat, ix->fail, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-    KNN_HIP(hipStreamSynchronize(st));
-    *nfail = ix->hstat[0];
-    std::memcpy(ratio, &ix->hstat[1], sizeof(float));
+    const int seq = ix->mail_seq;
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(&ix->mail[0], __ATOMIC_ACQUIRE) == seq) break;
+        if ((it & 255u) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(&ix->mail[0], __ATOMIC_ACQUIRE) == seq) break;
+                set_err("rerank finished without publishing its stats (seq %d)", seq);
+                return KNN_EHIP;
+            }
+            if (e != hipErrorNotReady) KNN_HIP(e);
+        }
+        __builtin_ia32_pause();
+    }
+    *nfail = __atomic_load_n(&ix->mail[1], __ATOMIC_ACQUIRE);
+    const int bits = __atomic_load_n(&ix->mail[2], __ATOMIC_ACQUIRE);
+    std::memcpy(ratio, &bits, sizeof(float));
     return KNN_OK;
 }
 
@@ -469,7 +512,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 2)) != KNN_OK) return rc;
+    if ((rc = grow_fail(ix, nq, st)) != KNN_OK) return rc;
     if (!q_ready)   // else search_locked's fused query prep already wrote qb16 / q_resid
         KNN_HIP(imgrec::launch_bf16_rows(qpad, p.nq_pad, ix->dp, ix->dpb, ix->qb16, ix->q_resid, st));
     TileArgs a{};
@@ -491,14 +534,13 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     KNN_HIP(imgrec::launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
                                             ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
                                             ix->mws_d, ix->mws_i, ix->mws_f, st));
-    KNN_HIP(hipMemsetAsync(ix->fail, 0, 2 * sizeof(int), st));
     imgrec::RerankArgs r{};
     r.mode = imgrec::kModeBF16;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = b16_acc_coef(ix->dpb);
-    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I; r.fail_count = ix->fail;
-    r.fail_list = ix->fail + 2; r.err_ratio = reinterpret_cast<float*>(ix->fail + 1);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+    bind_stats(ix, &r);
     r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
     KNN_HIP(imgrec::launch_rerank_certify(r, st));
     int nfail = 0;
@@ -508,7 +550,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     ix->last_split_queries += nq;
     if (nfail <= 0) return KNN_OK;
     ix->last_fallback += nfail;
-    return cascade(ix, qpad, qnorm, ix->fail + 2, nfail, k, D, I, st);
+    return cascade(ix, qpad, qnorm, ix->fail + 3, nfail, k, D, I, st);
 }
 
 // Split-bf16 candidates + exact rerank + certificate; uncertified queries re-run exactly.
@@ -524,7 +566,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq + 2)) != KNN_OK) return rc;
+    if ((rc = grow_fail(ix, nq, st)) != KNN_OK) return rc;
     KNN_HIP(imgrec::launch_split_rows(qpad, p.nq_pad, ix->dp, imgrec::kSplitBK, ix->qsplit, st));
     TileArgs a{};
     a.wr = p.wr; a.wq = p.wq; a.km = kc;
@@ -541,15 +583,13 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     // global top-K' approximate candidates, raw ascending keys (merge in its L2 convention)
     KNN_HIP(imgrec::launch_merge(ix->cand_d, ix->cand_i, nq, a.ncand / kc, kc, a.ncand, kc, kc, 1,
                                  0, ix->cand2_d, ix->cand2_i, st));
-    KNN_HIP(hipMemsetAsync(ix->fail, 0, 2 * sizeof(int), st));
     imgrec::RerankArgs r{};
     r.mode = imgrec::kModeSplit;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = split_coef(ix->dp);
-    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I; r.fail_count = ix->fail;
-    r.fail_list = ix->fail + 2;
-    r.err_ratio = reinterpret_cast<float*>(ix->fail + 1);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+    bind_stats(ix, &r);
     KNN_HIP(imgrec::launch_rerank_certify(r, st));
     int nfail = 0;
     float ratio = 0.f;
@@ -563,11 +603,11 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     if ((rc = grow(&ix->fb_qn, &ix->fb_qn_cap, (size_t)pf.nq_pad)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_d, &ix->fb_d_cap, (size_t)nfail * k)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_i, &ix->fb_i_cap, (size_t)nfail * k)) != KNN_OK) return rc;
-    KNN_HIP(imgrec::launch_gather_rows(qpad, qnorm, ix->dp, ix->fail + 2, nfail, pf.nq_pad, ix->fb_q,
+    KNN_HIP(imgrec::launch_gather_rows(qpad, qnorm, ix->dp, ix->fail + 3, nfail, pf.nq_pad, ix->fb_q,
                                        ix->fb_qn, st));
     if ((rc = exact_chunk(ix, ix->fb_q, ix->fb_qn, nfail, k, ix->fb_d, ix->fb_i, st, false)) != KNN_OK)
         return rc;
-    KNN_HIP(imgrec::launch_scatter_results(ix->fb_d, ix->fb_i, ix->fail + 2, nfail, k, D, I, st));
+    KNN_HIP(imgrec::launch_scatter_results(ix->fb_d, ix->fb_i, ix->fail + 3, nfail, k, D, I, st));
     return KNN_OK;
 }
 
@@ -689,7 +729,7 @@ int knn_free(knn_index_t* ix) {
                     (void*)ix->fb_q, (void*)ix->fb_qn, (void*)ix->fb_d, (void*)ix->fb_i,
                     (void*)ix->hq, (void*)ix->hd, (void*)ix->hi})
         if (p) (void)hipFree(p);
-    if (ix->hstat) (void)hipHostFree(ix->hstat);
+    if (ix->mail) (void)hipHostFree(ix->mail);
     for (hipEvent_t e : ix->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ix->stream);
     delete ix;

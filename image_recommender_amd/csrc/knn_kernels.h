@@ -55,9 +55,12 @@ struct RerankArgs {
                                 // have besides the K'-th candidate's (merge "floor"), or NULL
     float* D;
     int64_t* I;
-    int* fail_count;            // device counter (zeroed by the caller)
+    int* fail_count;            // device counter (zero before the first search; the stats
+                                // publish kernel after the rerank zeroes it and err_ratio again)
     int* fail_list;             // nq entries
     float* err_ratio;           // device max of observed error / bound (>= 0 floats, atomicMax)
+    int* mail;                  // host-mapped [seq, uncertified count, err_ratio bits]
+    int seq;                    // written to mail[0] last, once the two values are there
 };
 
 constexpr int kTileRowsMax = 256;   // corpus capacity is rounded to this many rows

@@ -371,13 +371,31 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
     if (floor) tau = fminf(tau, floor[q]);
     const float a_out = __shfl(ak, min(m, 63), 64);
     if (m < nvalid) tau = fminf(tau, a_out);
-    if (tau == INFINITY) return;
-    float sk = (inP && rank == k - 1) ? key : -INFINITY;
+    bool failed = false;                            // tau = +inf: every row was reranked
+    if (tau != INFINITY) {
+        float sk = (inP && rank == k - 1) ? key : -INFINITY;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
-    // fewer than k reranked rows while rows were left out: nothing to certify with
-    const bool certified = m >= k && (tau - bound_a(tau)) > (sk + bound_f(sk));
-    if (!certified && lane == 0) fail_list[atomicAdd(fail_count, 1)] = (int)q;
+        for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
+        // fewer than k reranked rows while rows were left out: nothing to certify with
+        failed = !(m >= k && (tau - bound_a(tau)) > (sk + bound_f(sk)));
+    }
+    if (failed && lane == 0) fail_list[atomicAdd(fail_count, 1)] = (int)q;
+}
+
+// After a rerank (the kernel boundary orders every workgroup's stats atomics before it): publish
+// the uncertified count and the error ratio to the host mailbox (pinned, mapped; the host spins
+// on mail[0] == seq instead of a device-to-host copy and a stream synchronisation) and zero the
+// counters for the next search.  One lane; vector stores only.
+__global__ void __launch_bounds__(64)
+publish_stats_kernel(int* __restrict__ fail_count, int* __restrict__ err_bits, int* __restrict__ mail,
+                     int seq) {
+    if (threadIdx.x != 0) return;
+    const int nf = *fail_count, er = *err_bits;
+    *fail_count = 0;
+    *err_bits = 0;
+    __hip_atomic_store(mail + 1, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(mail + 2, er, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(mail, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void __launch_bounds__(256)
@@ -434,7 +452,7 @@ hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32
 
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
-    if (a.kc > 64 || a.k > a.kc || a.dp % 4 != 0) return hipErrorInvalidValue;
+    if (a.kc > 64 || a.k > a.kc || a.dp % 4 != 0 || !a.mail) return hipErrorInvalidValue;
 #define IMGREC_RERANK(ITV)                                                                          \
     hipLaunchKernelGGL((rerank_certify_kernel<ITV>), dim3((unsigned)a.nq), dim3(kRerankWaves * 64), \
                        0, st, a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci,   \
@@ -445,6 +463,10 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     else if (a.dp <= 2048) IMGREC_RERANK(8);
     else IMGREC_RERANK(0);
 #undef IMGREC_RERANK
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(publish_stats_kernel, dim3(1), dim3(64), 0, st, a.fail_count,
+                       reinterpret_cast<int*>(a.err_ratio), a.mail, a.seq);
     return hipGetLastError();
 }
 
