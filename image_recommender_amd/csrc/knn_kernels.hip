@@ -177,6 +177,16 @@ __device__ __forceinline__ void dma16(const float* g, uint32_t lds) {
         "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
         : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
 }
+// The same with the non-temporal policy, for bf16 corpus rows that exactly one workgroup reads (a
+// launch with one query block): nq = 1 on 1M x 1968 0.695 -> 0.667 ms.  The fp32 corpus of the
+// exact kernel runs slower with it (1.94 -> 2.70 ms), so it keeps the default policy.
+__device__ __forceinline__ void dma16_nt(const float* g, uint32_t lds) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
 __device__ __forceinline__ void dma4(const float* g, uint32_t lds) {
     unsigned keep;
     asm volatile(
@@ -288,10 +298,16 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     int64_t poff[LPW];
     bool pis_a[LPW];
     uint32_t pdst[LPW];
+    bool pnt[LPW];                          // corpus piece of a one-query-block launch: read once
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
         const int pc = wave * LPW + j;
         pis_a[j] = pc < PA;
+#ifdef IMGREC_NO_NT
+        pnt[j] = false;
+#else
+        pnt[j] = MODE == kModeBF16 && pis_a[j] && nqb == 1;   // fp32 rows: 1.94 -> 2.70 ms at nq = 1
+#endif
         const int prow0 = pis_a[j] ? pc * RPP : (pc - PA) * RPP;
         poff[j] = (int64_t)prow0 * dp + (((prow0 / RPP) & 1) ? goff1 : goff0);
         pdst[j] = (uint32_t)(pis_a[j] ? pc * 256 : SA + (pc - PA) * 256) * 4u;
@@ -314,7 +330,8 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
 #ifdef IMGREC_ABLATE_A_ONLY
             if (pis_a[j])
 #endif
-            dma16((pis_a[j] ? itile : qbase) + poff[j] + k0, st + pdst[j]);
+            if (pnt[j]) dma16_nt(itile + poff[j] + k0, st + pdst[j]);
+            else dma16((pis_a[j] ? itile : qbase) + poff[j] + k0, st + pdst[j]);
         }
         if (++is == nsteps) { is = 0; ++it; itile += (size_t)nsplit * BM * dp; }
         ibuf = (ibuf + 1 == NS) ? 0 : ibuf + 1;
