@@ -283,3 +283,32 @@ def test_bf16_cluster_sorted_storage(faiss, nq):
     check_knn(D[sel], I[sel], xb, xq[sel], 10, "l2", min_exact_frac=0.5)
     print(f"cluster-sorted storage: {nfb} of {nq} queries re-run")
     assert nfb <= nq // 20
+
+
+def test_bf16_stats_mailbox_per_search(faiss):
+    """The certificate stats reach the host through a pinned mailbox and the device counters are
+    zeroed after every rerank: an all-failing search followed by a clean one reports 0 fallbacks,
+    and two indexes searched in turn keep their own counts (csrc/knn_refine.hip
+    publish_stats_kernel, csrc/knn_capi.cpp read_stats)."""
+    base = mixture(200, 256, centres=20, seed=19)
+    dup = faiss.IndexFlatL2(256)
+    dup.add(np.repeat(base, 80, axis=0))                 # 80 copies of each row: no certificate
+    dup.search_mode = "bf16"
+    clean = faiss.IndexFlatL2(256)
+    xc = mixture(9000, 256, centres=60, seed=20)
+    clean.add(xc)
+    clean.search_mode = "bf16"
+    qd = base[:40] + np.float32(1e-3)
+    qc = mixture(200, 256, centres=60, seed=21)
+    for _ in range(3):
+        dup.search(qd, 10)
+        assert tuple(dup.search_stats()) == (40, 40)
+        D, I = clean.search(qc, 10)
+        ncand, nfb = clean.search_stats()
+        assert ncand == 200 and nfb <= 4
+        _bound_holds(clean)
+        check_knn(D, I, xc, qc, 10, "l2", min_exact_frac=0.5)
+    D, I = dup.search(qd, 10)
+    assert (I == np.arange(40)[:, None] * 80 + np.arange(10)[None, :]).all()
+    dup.search(qd[:1], 10)
+    assert tuple(dup.search_stats()) == (1, 1)
