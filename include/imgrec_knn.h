@@ -26,9 +26,10 @@
  *   - Host-pointer functions (knn_add, knn_search, knn_write, ...) synchronise before returning.
  *     *_device functions take device pointers and a hipStream_t (passed as void*; NULL = the
  *     HIP null stream, like any HIP API) and enqueue asynchronously; they allocate only when the
- *     workspace must grow.  knn_search_device synchronises its stream once per call on the
- *     candidate paths (bf16 / split): the host reads the uncertified-query count (8 bytes) to
- *     decide the re-run; the exact path never synchronises.
+ *     workspace must grow.  knn_search_device waits once per call on the candidate paths
+ *     (bf16 / split) for the uncertified-query count, which a one-lane kernel after the rerank
+ *     writes into a pinned host mailbox (the host polls it; no copy, no stream synchronisation),
+ *     to decide the re-run; the exact path never waits.
  *   - Vectors are row-major float32, n rows × d.  Labels are int64.  Result rows are sorted by
  *     ascending distance (L2) or descending inner product (IP/COSINE); exact ties are broken by the
  *     smaller label.  When fewer than k vectors exist, the tail of a result row holds label -1 and
@@ -73,7 +74,7 @@ enum knn_error {
  *       the batch is large; everything else the exact fp32 kernel.
  * EXACT: always the fp32 kernel.  SPLIT: the split path (bf16 hi/lo, three MFMAs per product,
  *       K' = 16/32) whenever k <= 16 and d >= 256.  BF16: the bf16 path for every batch (tests).
- * A candidate-path search synchronises its stream once per 8192-query chunk (certificate count). */
+ * A candidate-path search waits once per 8192-query chunk for its certificate count. */
 enum knn_search_mode {
     KNN_SEARCH_AUTO = 0,
     KNN_SEARCH_EXACT = 1,
