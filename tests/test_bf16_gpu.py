@@ -312,3 +312,18 @@ def test_bf16_stats_mailbox_per_search(faiss):
     assert (I == np.arange(40)[:, None] * 80 + np.arange(10)[None, :]).all()
     dup.search(qd[:1], 10)
     assert tuple(dup.search_stats()) == (1, 1)
+
+
+def test_bf16_two_query_chunks(faiss):
+    """9000 queries = two 8192-query chunks, each with its own candidate pass, rerank and mailbox
+    wait; the certificate counts add up over the chunks and the rows at the seam are exact."""
+    xb = mixture(20000, 256, centres=90, seed=61)
+    xq = mixture(9000, 256, centres=90, seed=62)
+    idx = faiss.IndexFlatL2(256)
+    idx.add(xb)
+    D, I = idx.search(xq, 10)                             # AUTO: bf16 for this batch and corpus
+    ncand, nfb = idx.search_stats()
+    assert ncand == 9000 and nfb <= 450
+    _bound_holds(idx)
+    sel = np.r_[0:30, 8170:8215, 8980:9000]
+    check_knn(D[sel], I[sel], xb, xq[sel], 10, "l2", min_exact_frac=0.5)
