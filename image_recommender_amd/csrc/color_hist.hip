@@ -13,6 +13,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -152,43 +153,67 @@ color_hist_fixed_kernel(const uint8_t* __restrict__ pix, const int64_t* __restri
                         const int64_t* __restrict__ npix, float* __restrict__ out,
                         uint32_t* __restrict__ counts) {
     constexpr int nb = 3 * BINS;
-    __shared__ __attribute__((aligned(16))) uint32_t hist[nb * NT];   // [3*BINS][NT]
+    // u32 counters: a thread would need 2^32 bytes of one bin to overflow.  (16-bit counters,
+    // two bins per word with a fold every 1365 granules, doubled the workgroups per CU and ran
+    // no faster — 4.40-4.48 vs 4.39-4.52 TB/s — so the per-CU LDS atomic rate, not occupancy,
+    // bounds this kernel; profiles/r01_ab_color/.)  A chunk loop with a fold between chunks is
+    // kept for such a counter format.
+    constexpr int nw = nb;
+    constexpr int64_t chunk = INT64_MAX / 64;
+    __shared__ __attribute__((aligned(16))) uint32_t hist[nw * NT];   // [word][NT]
+    __shared__ uint32_t tot32[nb];
     __shared__ float tot[nb];
     const int tid = threadIdx.x;
-    for (int i = tid; i < nb * NT; i += NT) hist[i] = 0u;
+    for (int i = tid; i < nw * NT; i += NT) hist[i] = 0u;
+    if (tid < nb) tot32[tid] = 0u;
     __syncthreads();
 
     const int64_t img = blockIdx.x;
     const int64_t nbytes = 3 * npix[img];
     const uint8_t* base = pix + offsets[img];
     uint32_t* col = hist + tid;
+    const int lane = tid & 63, wave = tid >> 6;
     auto count1 = [&](int64_t o) {                      // one byte at image offset o
         const int ch = (int)(o % 3);
         const uint32_t bin = ((uint32_t)base[o] * (uint32_t)BINS) >> 8;
         atomicAdd(col + (ch * BINS + (int)bin) * NT, 1u);
     };
+    // columns -> tot32 (and zeroed for the next chunk): wave w folds words w, w + 4, ...
+    auto fold = [&]() {
+        __syncthreads();
+        for (int wd = wave; wd < nw; wd += NT / 64) {
+            uint32_t* row = hist + wd * NT;
+            const uint32_t v0 = row[lane], v1 = row[lane + 64], v2 = row[lane + 128], v3 = row[lane + 192];
+            row[lane] = 0u; row[lane + 64] = 0u; row[lane + 128] = 0u; row[lane + 192] = 0u;
+            uint32_t sm = v0 + v1 + v2 + v3;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+            if (lane == 0) tot32[wd] += sm;
+        }
+        __syncthreads();
+    };
+
     const int64_t head = std::min<int64_t>(nbytes, (int64_t)((16 - ((uintptr_t)base & 15)) & 15));
     if (tid < head) count1(tid);
     const int64_t ngran = (nbytes - head) / 48;
     const uint4* vb = reinterpret_cast<const uint4*>(base + head);
-    switch ((int)(head % 3)) {                          // uniform over the workgroup
-        case 0: count_body<BINS, 0>(col, vb, ngran, tid); break;
-        case 1: count_body<BINS, 1>(col, vb, ngran, tid); break;
-        default: count_body<BINS, 2>(col, vb, ngran, tid); break;
+    const int phase = (int)(head % 3);                  // uniform over the workgroup
+    for (int64_t g0 = 0; g0 < ngran; g0 += chunk) {
+        const int64_t ng = std::min<int64_t>(ngran - g0, chunk);
+        const uint4* v = vb + 3 * g0;
+        switch (phase) {
+            case 0: count_body<BINS, 0>(col, v, ng, tid); break;
+            case 1: count_body<BINS, 1>(col, v, ng, tid); break;
+            default: count_body<BINS, 2>(col, v, ng, tid); break;
+        }
+        if (g0 + chunk < ngran) fold();
     }
     for (int64_t o = head + 48 * ngran + tid; o < nbytes; o += NT) count1(o);   // < 48 bytes
-    __syncthreads();
+    fold();
 
-    const int lane = tid & 63, wave = tid >> 6;
-    for (int b = wave; b < nb; b += NT / 64) {
-        const uint32_t* row = hist + b * NT;
-        uint32_t s = row[lane] + row[lane + 64] + row[lane + 128] + row[lane + 192];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (lane == 0) {
-            tot[b] = (float)s;
-            if (counts) counts[img * nb + b] = s;
-        }
+    if (tid < nb) {
+        tot[tid] = (float)tot32[tid];
+        if (counts) counts[img * nb + tid] = tot32[tid];
     }
     __syncthreads();
     if (wave == 0) {

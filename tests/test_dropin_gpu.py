@@ -174,3 +174,16 @@ def test_color_histogram_fixed_bins_alignments(gpu):
     for im, h, c in zip(imgs, out, counts):
         np.testing.assert_array_equal(c, color_counts(im, 16))
         np.testing.assert_allclose(h, color_hist_reference(im, 16), rtol=1e-6, atol=1e-9)
+
+
+def test_color_histogram_large_image(gpu):
+    """An 18 MB image: more bytes per thread than a 16-bit counter holds (the fixed-bin kernel
+    built with 16-bit counters folds its columns between chunks); counts exact."""
+    from image_recommender_amd.vector_scripts.create_color_vector import color_histograms
+    from oracle.color_hist import color_counts
+    rng = np.random.default_rng(78)
+    big = rng.integers(0, 256, (2500, 2400, 3), dtype=np.uint8)
+    big[:1200, :, 0] = 3                                              # a heavily skewed channel
+    out, counts = color_histograms([big, big[:1, :5]], bins=16, return_counts=True)
+    np.testing.assert_array_equal(counts[0], color_counts(big, 16))
+    np.testing.assert_array_equal(counts[1], color_counts(big[:1, :5], 16))
