@@ -217,7 +217,12 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
     for (int p = 0; p < K; ++p) c[p] = d < kd[p];
 #pragma unroll
     for (int p = K - 1; p > 0; --p) {
+#ifdef IMGREC_NO_MED3
         kd[p] = c[p - 1] ? kd[p - 1] : (c[p] ? d : kd[p]);
+#else
+        // the same select on an ascending list is the median of (kd[p-1], d, kd[p]): one v_med3
+        kd[p] = __builtin_amdgcn_fmed3f(kd[p - 1], d, kd[p]);
+#endif
         ki[p] = c[p - 1] ? ki[p - 1] : (c[p] ? id : ki[p]);
     }
     kd[0] = c[0] ? d : kd[0];
