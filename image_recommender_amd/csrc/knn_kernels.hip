@@ -818,7 +818,7 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
             v[p] = lab < 0 ? kEmpty
                            : ((uint64_t)key_bits_ordered(kv) << 32) | (uint32_t)(lab - id_offset);
         }
-        if (ip[KIN - 1] >= 0) fl = lp[KIN - 1];                 // a full list: its last key
+        if (ip[KIN - 1] >= 0) fl = fminf(fl, lp[KIN - 1]);      // a full list: its last key
     } else {
 #pragma unroll
         for (int p = 0; p < KIN; ++p) v[p] = kEmpty;
@@ -945,9 +945,11 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
         if (kin == 8) IMGREC_CAND_LANE(8, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
         else if (kin == 10) IMGREC_CAND_LANE(10, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
         else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
-#undef IMGREC_CAND_LANE
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+// (the same threshold select at level 2 — cand_merge_lane_kernel<64>, a group's 64 outputs per
+// lane — measured 32.5 us per query at nq = 1, no faster than this queue merge's 31 us)
+#undef IMGREC_CAND_LANE
         hipLaunchKernelGGL(cand_merge_lds_kernel, dim3((unsigned)nq), dim3(64), 0, st, ws_d, ws_i, nq,
                            G, kout, kout, id_offset, ws_floor, D, I, floor);
         return hipGetLastError();
