@@ -947,8 +947,11 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
         else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-// (the same threshold select at level 2 — cand_merge_lane_kernel<64>, a group's 64 outputs per
-// lane — measured 32.5 us per query at nq = 1, no faster than this queue merge's 31 us)
+        // Level 2 (the G group outputs) is the LDS queue merge, 31 us per query at nq = 1.
+        // Measured and dropped: the threshold select with a group's 64 outputs per lane
+        // (cand_merge_lane_kernel<64>, 32.5 us), reading each queue's next entry one pop ahead
+        // (32.3 us), and a 256-thread rank form (binary searches of every entry in every other
+        // queue, 123 us: dependent LDS reads per thread).
 #undef IMGREC_CAND_LANE
         hipLaunchKernelGGL(cand_merge_lds_kernel, dim3((unsigned)nq), dim3(64), 0, st, ws_d, ws_i, nq,
                            G, kout, kout, id_offset, ws_floor, D, I, floor);
