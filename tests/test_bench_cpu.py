@@ -1,0 +1,42 @@
+"""Host logic of bench.py (no GPU): which committed PMC records the bench line cites.
+
+The bench attaches `roofline.traffic` (rocprofv3 FETCH_SIZE/WRITE_SIZE passes) and the clock /
+MFMA-busy record from the newest `profiles/r01_v*` files whose kernel name matches the kernel the
+search ran; a stale or mismatched file would put another kernel's bytes on the line."""
+import json
+import re
+
+import bench
+
+
+def test_kernel_pattern_names_the_bf16_tile_kernel():
+    name, pat = bench.kernel_pattern(256, 256, 2, 10)
+    assert name == "knn_b16_tile_kernel<10, 1>"
+    assert re.search(pat, "void imgrec::knn_b16_tile_kernel<10, 1>")
+    name, pat = bench.kernel_pattern(256, 32, 2, 10)             # small-batch generic kernel
+    assert re.search(pat, "void imgrec::knn_tile_topk_kernel<2, 1, 16, 2, 32, 2, 4>")
+    assert not re.search(pat, "void imgrec::knn_b16_tile_kernel<10, 1>")
+
+
+def test_pmc_records_are_the_newest_matching(tmp_path, monkeypatch):
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    kern = "void imgrec::knn_b16_tile_kernel<10, 1>"
+    for v, b in ((7, 1.0), (16, 2.0), (9, 3.0)):
+        (prof / f"r01_v{v}_traffic.json").write_text(json.dumps({kern: {"hbm_bytes_per_launch": b}}))
+    (prof / "r01_v20_traffic.json").write_text(json.dumps({"other_kernel": {"hbm_bytes_per_launch": 9.0}}))
+    (prof / "r01_v16_clock.json").write_text(json.dumps({kern: {"clock_ghz": 1.7, "mfma_busy": 0.5}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    _, pat = bench.kernel_pattern(256, 256, 2, 10)
+    assert bench.pmc_traffic(pat) == (2.0, "r01_v16_traffic.json")
+    rec, f = bench.pmc_record(pat, "_clock.json")
+    assert f == "r01_v16_clock.json" and rec["clock_ghz"] == 1.7
+    assert bench.pmc_traffic(r"no_such_kernel") is None
+
+
+def test_committed_records_cover_the_bench_kernel():
+    _, pat = bench.kernel_pattern(256, 256, 2, 10)
+    bytes_, src = bench.pmc_traffic(pat)
+    assert src == "r01_v16_traffic.json" and 5e9 < bytes_ < 7e9     # 1.5x the 3.97 GB bf16 corpus
+    rec, src = bench.pmc_record(pat, "_clock.json")
+    assert src == "r01_v16_clock.json" and 0.0 < rec["mfma_busy"] < 1.0
