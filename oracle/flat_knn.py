@@ -43,18 +43,20 @@ def search_exact(xb: np.ndarray, xq: np.ndarray, k: int, metric: str = "l2",
     """Exact k-NN in float64.  Returns (D float64 (nq,k), I int64 (nq,k)) in faiss conventions.
 
     metric: "l2" (IndexFlatL2), "ip" (IndexFlatIP), "cosine" (rows and queries normalised, IP).
+    Rows are converted to float64 one block at a time, so a float32 corpus of any size is only
+    copied block by block (the full-size config-3/4 tests check 1M+ rows this way).
     """
-    xb = np.asarray(xb, dtype=np.float64)
     xq = np.asarray(xq, dtype=np.float64)
     if metric == "cosine":
-        xb = _normalize64(xb)
         xq = _normalize64(xq)
     nq, n = xq.shape[0], xb.shape[0]
     bestk = np.full((nq, k), np.inf)
     besti = np.full((nq, k), -1, dtype=np.int64)
     qn = (xq * xq).sum(1)
     for r0 in range(0, n, block):
-        xc = xb[r0:r0 + block]
+        xc = np.asarray(xb[r0:r0 + block], dtype=np.float64)
+        if metric == "cosine":
+            xc = _normalize64(xc)
         ip = xq @ xc.T
         if metric == "l2":
             keys = qn[:, None] + (xc * xc).sum(1)[None, :] - 2.0 * ip

@@ -30,11 +30,14 @@ def _exact_pair(xb, xq, qi, ids, metric):
     return x @ q
 
 
-def check_knn(D, I, xb, xq, k, metric="l2", min_exact_frac=0.0):
+def check_knn(D, I, xb, xq, k, metric="l2", min_exact_frac=0.0, oracle=None):
+    """oracle: optional precomputed search_exact(xb, xq, k + 1, metric) (reused by tests that check
+    several searches of one large corpus)."""
     D = np.asarray(D, dtype=np.float64)
     I = np.asarray(I)
     n = xb.shape[0]
-    Dg, Ig = search_exact(xb, xq, k + 1, metric)
+    Dg, Ig = oracle if oracle is not None else search_exact(xb, xq, k + 1, metric)
+    assert Dg.shape[1] >= k + 1
     assert D.shape == (xq.shape[0], k) and I.shape == (xq.shape[0], k)
     checked = total = 0
     for q in range(xq.shape[0]):
