@@ -28,6 +28,8 @@ _pi64, _pf, _pi, _pd = C.POINTER(C.c_int64), C.POINTER(C.c_float), C.POINTER(C.c
 SIGNATURES = {
     # imgrec_knn.h
     "knn_create": (_i, [_i, _i, _i, C.POINTER(_vp)]),
+    "knn_create_multi": (_i, [_i, _i, _pi, _i, C.POINTER(_vp)]),
+    "knn_num_shards": (_i, [_vp]),
     "knn_free": (_i, [_vp]),
     "knn_dim": (_i, [_vp]),
     "knn_metric": (_i, [_vp]),
@@ -50,12 +52,14 @@ SIGNATURES = {
     "ivfpq_scan_device": (_i, [_vp, _vp, _i64, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "knn_write": (_i, [_vp, C.c_char_p]),
     "knn_read": (_i, [C.c_char_p, _i, C.POINTER(_vp)]),
+    "knn_read_multi": (_i, [C.c_char_p, _pi, _i, C.POINTER(_vp)]),
     "knn_normalize_L2": (_i, [_vp, _i64, _i]),
     "knn_set_timing": (_i, [_vp, _i]),
     "knn_kernel_time": (_i, [_vp, _pd, _pi]),
     "knn_plan": (_i, [_vp, _i64, _i, _pi, _pi, _pi, _pi]),
     "knn_set_search_mode": (_i, [_vp, _i]),
     "knn_search_stats": (_i, [_vp, _pi64, _pi64, _pf]),
+    "knn_search_stats2": (_i, [_vp, _pi64, _pi64, _pi64, _pf]),
     "knn_last_path": (_i, [_vp]),
     "knn_last_error": (C.c_char_p, []),
     "knn_version": (C.c_char_p, []),

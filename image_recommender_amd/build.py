@@ -3,7 +3,8 @@
 One C-ABI shared library holds every native piece of the hot path (no torch types anywhere in its
 signatures):
 
-* ``csrc/knn_kernels.hip`` + ``csrc/knn_capi.cpp`` — the exact k-NN index (include/imgrec_knn.h)
+* ``csrc/knn_*.hip`` + ``csrc/knn_{capi,plan,search,multi,io}.cpp`` — the exact k-NN index
+  (include/imgrec_knn.h), ``csrc/ivfpq.hip`` + ``ivfpq_capi.cpp`` — IVF-PQ (include/imgrec_ivfpq.h)
 * ``csrc/color_hist.hip`` — the per-image colour histogram (include/imgrec_color.h)
 * ``csrc/ingest.cpp`` — the SQLite pickle-BLOB fast path (include/imgrec_ingest.h)
 
@@ -28,10 +29,11 @@ LIB = LIBDIR / os.environ.get("IMGREC_LIB_NAME", "libimgrec.so")
 EXTRA_FLAGS = os.environ.get("IMGREC_EXTRA_FLAGS", "").split()
 ARCH = os.environ.get("IMGREC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_refine.hip", "knn_capi.cpp", "color_hist.hip", "ingest.cpp",
-           "ivfpq.hip"]
-HEADERS = ["knn_kernels.h", "wave_ops.h", "../../include/imgrec_ivfpq.h", "../../include/imgrec_knn.h", "../../include/imgrec_color.h",
-           "../../include/imgrec_ingest.h"]
+SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_refine.hip", "knn_capi.cpp", "knn_plan.cpp",
+           "knn_search.cpp", "knn_multi.cpp", "knn_io.cpp", "ivfpq_capi.cpp", "color_hist.hip",
+           "ingest.cpp", "ivfpq.hip"]
+HEADERS = ["knn_kernels.h", "knn_index.h", "knn_multi.h", "wave_ops.h", "../../include/imgrec_ivfpq.h",
+           "../../include/imgrec_knn.h", "../../include/imgrec_color.h", "../../include/imgrec_ingest.h"]
 
 
 def _hipcc() -> str:

@@ -91,6 +91,9 @@ bool parse(const uint8_t* blob, int64_t len, const uint8_t** payload, int64_t* n
     int nd = 0;
     while (c.ok && c.need(1) && (*c.p == 0x4b || *c.p == 0x4d || *c.p == 0x4a) && nd < 3) {
         if (!c.small_int(&v)) return false;
+        // a shape holding more elements than the payload is rejected before the product can
+        // overflow (shape ints come from an untrusted BLOB; found by tests/test_ingest_fuzz_cpu.py)
+        if (v > 0 && prod > (int64_t)(nb / 4) / v) return false;
         prod *= v;
         ++nd;
     }

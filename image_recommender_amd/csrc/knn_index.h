@@ -1,0 +1,170 @@
+// knn_index.h — internal state of one k-NN index and the helpers the C-ABI translation units
+// share (knn_capi.cpp: entry points; knn_plan.cpp: launch geometry and error-bound coefficients;
+// knn_search.cpp: the search paths; knn_io.cpp: the faiss file layout; knn_multi.cpp: one index
+// over several devices).  Not part of the public ABI (include/imgrec_knn.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/imgrec_knn.h"
+#include "knn_kernels.h"
+
+namespace imgrec {
+
+void set_err(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define KNN_FAIL(code, ...)              \
+    do {                                 \
+        ::imgrec::set_err(__VA_ARGS__);  \
+        return (code);                   \
+    } while (0)
+
+#define KNN_HIP(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ::imgrec::set_err("%s failed: %s", #expr, hipGetErrorString(e_));          \
+            return e_ == hipErrorOutOfMemory ? KNN_ENOMEM : KNN_EHIP;                  \
+        }                                                                              \
+    } while (0)
+
+struct DeviceGuard {
+    int old = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&old) != hipSuccess) old = -1;
+        if (dev >= 0 && dev != old) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (old >= 0 && hipGetDevice(&cur) == hipSuccess && cur != old) (void)hipSetDevice(old);
+    }
+};
+
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// Device buffer that only grows (workspace reused across searches).
+template <typename T>
+int grow(T** p, size_t* cap, size_t need) {
+    if (*cap >= need) return KNN_OK;
+    const size_t n = std::max(need, *cap * 3 / 2);
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    KNN_HIP(hipMalloc((void**)p, n * sizeof(T)));
+    *cap = n;
+    return KNN_OK;
+}
+
+// ---- launch geometry (knn_plan.cpp; DESIGN.md "Launch plan") ---------------------------------
+struct Plan {
+    int wr, wq, km, bm, bq;
+    int nqb, nq_pad, ntiles, nsplit, ncand, wgs;
+    bool big;                    // bf16 path: the 256 x 256-tile kernel (knn_b16.hip)
+};
+constexpr int64_t kQueryChunk = 8192;
+Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus);
+Plan make_split_plan(int64_t ntotal, int64_t nq, int kc, int cus);
+Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus, int dpb);
+// The exact re-run of uncertified queries: the (2,1) tile of make_plan (256 rows x 32 queries)
+// on a fixed grid, planned on device for whatever count the certificate leaves.
+constexpr int kFallbackWR = 2;                 // lists per row split = 2 * kFallbackWR
+int fallback_km(int k);
+int fallback_grid(int cus, int64_t chunk_q);
+int split_kc(int k);
+float split_coef(int dp);
+float rerank_coef(int dp);
+float b16_acc_coef(int dpb);
+constexpr int kB16Cand = 64;                   // K': candidates the bf16 pass hands to the rerank
+int b16_km(int k);
+
+}  // namespace imgrec
+
+struct knn_index {
+    int d = 0, dp = 0, metric = KNN_METRIC_L2, device = 0, cus = 256;
+    int64_t ntotal = 0, cap = 0, id_offset = 0;
+    bool trained = true;
+    float* xb = nullptr;     // cap x dp
+    float* xn = nullptr;     // cap
+    uint32_t* xs = nullptr;  // cap x dp split-bf16 copy (split_ok only)
+    uint16_t* xh = nullptr;  // cap x dpb bf16 copy (b16_ok only)
+    float* xr = nullptr;     // cap: |x - bf16(x)| per row (b16_ok only)
+    float* xn_max = nullptr; // device scalar, max |x|^2 (refreshed when rows change)
+    float* xr_max = nullptr; // device scalar, max |x - bf16(x)|
+    int dpb = 0;             // bf16 row stride (elements)
+    bool split_ok = false, b16_ok = false, xn_max_stale = true;
+    int mode = KNN_SEARCH_AUTO;
+    int last_path = 0;       // knn_last_path
+    int64_t last_split_queries = 0;   // queries of the last search on a candidate path
+    hipStream_t stream = nullptr;     // the index's own stream (host-pointer entry points)
+    std::mutex mu;
+    // Cross-stream ordering: every operation enqueued on the index records `fence` on its stream;
+    // an operation on a different stream first waits for it (adds before searches, one search's
+    // workspace use before the next's, ...).
+    hipEvent_t fence = nullptr;
+    hipStream_t fence_stream = nullptr;
+    bool fence_set = false;
+    // search workspace
+    float* qpad = nullptr; size_t qpad_cap = 0;
+    float* qnorm = nullptr; size_t qnorm_cap = 0;
+    size_t xn_max_cap = 0;
+    float* cand_d = nullptr; size_t cand_d_cap = 0;
+    int64_t* cand_i = nullptr; size_t cand_i_cap = 0;
+    uint32_t* qsplit = nullptr; size_t qsplit_cap = 0;
+    float* cand2_d = nullptr; size_t cand2_d_cap = 0;
+    int64_t* cand2_i = nullptr; size_t cand2_i_cap = 0;
+    int* fail = nullptr; size_t fail_cap = 0;          // the uncertified queries of a chunk
+    int* stat = nullptr;                               // 12 ints: two chunk parities + totals
+    int stat_seq = 0;                                  // chunks run (parity = seq & 1)
+    bool stat_valid = false;                           // the last search ran a candidate path
+    uint16_t* qb16 = nullptr; size_t qb16_cap = 0;
+    float* q_resid = nullptr; size_t q_resid_cap = 0;
+    float* floor = nullptr; size_t floor_cap = 0;
+    float* mws_d = nullptr; size_t mws_d_cap = 0;          // two-level candidate merge workspace
+    int64_t* mws_i = nullptr; size_t mws_i_cap = 0;
+    float* mws_f = nullptr; size_t mws_f_cap = 0;
+    size_t xr_max_cap = 0;
+    // exact re-run workspace (device-planned: queries, candidate lists, plan)
+    float* fb_q = nullptr; size_t fb_q_cap = 0;
+    float* fb_qn = nullptr; size_t fb_qn_cap = 0;
+    float* fb_cd = nullptr; size_t fb_cd_cap = 0;
+    int64_t* fb_ci = nullptr; size_t fb_ci_cap = 0;
+    int* fb_dyn = nullptr;
+    // host-path staging
+    float* hq = nullptr; size_t hq_cap = 0;
+    float* hd = nullptr; size_t hd_cap = 0;
+    int64_t* hi = nullptr; size_t hi_cap = 0;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev;   // pairs
+    size_t ev_used = 0;
+    // one index over several devices (knn_multi.cpp); NULL for a single-device index
+    struct knn_multi* multi = nullptr;
+};
+
+namespace imgrec {
+
+// knn_capi.cpp
+const char* last_error();
+int set_metric(knn_index* ix, int metric);
+int set_trained(knn_index* ix, bool trained);
+int fence_begin(knn_index* ix, hipStream_t st);
+int fence_end(knn_index* ix, hipStream_t st);
+int reserve_rows(knn_index* ix, int64_t need, hipStream_t st);
+int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st);
+int create_single(int d, int metric, int device, knn_index** out);
+void free_single(knn_index* ix);
+// knn_search.cpp
+int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
+                  hipStream_t st);
+int read_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int64_t* first_fail,
+                      float* ratio);
+bool use_b16(const knn_index* ix, int64_t nq, int k);
+bool use_split(const knn_index* ix, int64_t nq, int k);
+
+}  // namespace imgrec

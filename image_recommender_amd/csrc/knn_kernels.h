@@ -30,6 +30,11 @@ struct TileArgs {
     float* cand_d;              // nq x ncand keys
     int64_t* cand_i;            // nq x ncand labels
     int ncand;
+    // device-planned launch (the exact re-run of uncertified queries): when set, the kernel reads
+    // {nq, nqb, nsplit, ncand} from dyn[0..3] and the grid has `grid` workgroups, those beyond
+    // nqb * nsplit exiting at once
+    const int* dyn = nullptr;
+    int grid = 0;
 };
 
 // One rerank + certificate launch over merged candidate-pass candidates (knn_refine.hip).
@@ -55,12 +60,16 @@ struct RerankArgs {
                                 // have besides the K'-th candidate's (merge "floor"), or NULL
     float* D;
     int64_t* I;
-    int* fail_count;            // device counter (zero before the first search; the stats
-                                // publish kernel after the rerank zeroes it and err_ratio again)
-    int* fail_list;             // nq entries
-    float* err_ratio;           // device max of observed error / bound (>= 0 floats, atomicMax)
-    int* mail;                  // host-mapped [seq, uncertified count, err_ratio bits]
-    int seq;                    // written to mail[0] last, once the two values are there
+    int* stats;                 // this chunk's device counters (zero on entry): [0] queries left
+                                // for the exact re-run, [1] max observed error / bound (float
+                                // bits, atomicMax), [2] queries whose first certificate failed
+    int* fail_list;             // nq entries: the queries left for the exact re-run
+    // the candidate pass's raw per-split lists (second chance; NULL = none): raw_lists sorted
+    // lists of raw_km entries per query, query q's at q * raw_stride_q (global labels, -1 empty)
+    const float* raw_d = nullptr;
+    const int64_t* raw_i = nullptr;
+    int raw_lists = 0, raw_km = 0;
+    int64_t raw_stride_q = 0;
 };
 
 constexpr int kTileRowsMax = 256;   // corpus capacity is rounded to this many rows
@@ -127,10 +136,27 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
                                    int64_t id_offset, float* D, int64_t* I, float* floor,
                                    float* ws_d, int64_t* ws_i, float* ws_floor, hipStream_t st);
 hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStream_t st);
+// multi-device index: dst[i] = start + i, and labels through a shard's local -> global map
+// (I[i] = lmap[I[i]] + offset, -1 kept)
+hipError_t launch_iota64(int64_t* dst, int64_t n, int64_t start, hipStream_t st);
+hipError_t launch_map_labels(int64_t* I, int64_t n, const int64_t* lmap, int64_t offset,
+                             hipStream_t st);
 
 hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32_t* dst,
                              hipStream_t st);
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st);
+// Plan + query gather of the device-side exact re-run (knn_refine.hip fallback_prep_kernel):
+// stat = 3 x 4 ints (two chunk parities + the search accumulators), list = the uncertified
+// queries; fq/fqn hold cap_rows rows (cap_rows >= the chunk's queries rounded up to 32);
+// lists_km = candidate lists per row split x their length.
+hipError_t launch_fallback_prep(int* stat, int parity, int first, const int* list, const float* qpad,
+                                const float* qnorm, int dp, int grid_wgs, int ntiles, int lists_km,
+                                int64_t cap_rows, float* fq, float* fqn, int* dyn, hipStream_t st);
+// Merge of a device-planned launch's lists (nq, nlists, stride from dyn, grid cap_q queries) with
+// the results scattered to rows out_rows[q] of D, I.
+hipError_t launch_merge_dyn(const float* cd, const int64_t* ci, const int* dyn, int lists_per_split,
+                            int kin, int64_t cap_q, int k, int metric, const int* out_rows,
+                            float* D, int64_t* I, hipStream_t st);
 hipError_t launch_gather_rows(const float* src, const float* src_norm, int dp, const int* list,
                               int64_t n, int64_t n_pad, float* dst, float* dst_norm, hipStream_t st);
 hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int* list, int64_t n,

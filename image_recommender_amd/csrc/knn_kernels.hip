@@ -240,7 +240,8 @@ __global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
                      int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
                      int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
-                     float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand) {
+                     float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand,
+                     const int* __restrict__ dyn) {
     using G = TileGeom<WR, WQ, NS, BK, WB>;
     constexpr int RW = G::RW;
     constexpr int NW = G::NW, BM = G::BM, BQ = G::BQ, SA = G::SA, STAGE = G::STAGE;
@@ -256,6 +257,14 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     const int nwg = gridDim.x, wg = blockIdx.x;
     const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
+    if (dyn) {                              // device-planned launch (exact re-run)
+        nq = dyn[0];
+        nqb = dyn[1];
+        nsplit = dyn[2];
+        ncand = dyn[3];
+        if (nq <= 0) return;
+    }
+    if (wgid >= nqb * nsplit) return;       // only a device-planned grid has spare workgroups
     const int qb = wgid % nqb;
     const int split = wgid / nqb;
     // this split's tiles, in increasing order: tile(j) for j in [0, t1).  Round-robin (split s
@@ -583,8 +592,14 @@ __global__ void __launch_bounds__(256)
 knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
                  int nlists, int kin, int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
                  int metric, int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
-                 float* __restrict__ floor_out) {
+                 float* __restrict__ floor_out, const int* __restrict__ dyn, int dyn_lists,
+                 const int* __restrict__ out_rows) {
     constexpr int QPB = 4 / WPQ;                     // queries per 256-thread block
+    if (dyn) {                                       // device-planned lists (exact re-run)
+        nq = dyn[0];
+        nlists = dyn[2] * dyn_lists;
+        stride_q = dyn[3];
+    }
     __shared__ float sd[4][KM];
     __shared__ int64_t si[4][KM];
     const int lane = threadIdx.x & 63;
@@ -638,7 +653,10 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
             for (int off = 32; off > 0; off >>= 1) floor_v = fminf(floor_v, __shfl_xor(floor_v, off, 64));
             if (active && lane == 0) floor_out[q] = floor_v;
         }
-        if (active) wave_select<KM>(kd, ki, k, lane, D + q * k, I + q * k, 1, metric);
+        if (active) {
+            const int64_t orow = out_rows ? (int64_t)out_rows[q] : q;
+            wave_select<KM>(kd, ki, k, lane, D + orow * k, I + orow * k, 1, metric);
+        }
         return;
     }
     // WPQ == 4: one query per block; every wave's top-k to LDS, wave 0 merges the 4k.
@@ -655,7 +673,8 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
             list_insert<KM, int64_t>(kd, ki, d, id);
         }
     }
-    wave_select<KM>(kd, ki, k, lane, D + q * k, I + q * k, 1, metric);
+    const int64_t orow = out_rows ? (int64_t)out_rows[q] : q;
+    wave_select<KM>(kd, ki, k, lane, D + orow * k, I + orow * k, 1, metric);
 }
 
 __global__ void fill_empty_kernel(float* __restrict__ D, int64_t* __restrict__ I, int64_t n,
@@ -678,11 +697,11 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
 
 template <int WR, int WQ, int NS, int BK, int MODE = kModeF32, int WB = 4>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
-    const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
+    const dim3 grid((unsigned)(a.dyn ? a.grid : a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
     hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, MODE, WB>), grid, block, 0, st, a.xb, \
                        a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
-                       a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
+                       a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand, a.dyn)
     switch (km) {
         case 8: IMGREC_LAUNCH_TILE(8); break;
         case 10: IMGREC_LAUNCH_TILE(10); break;
@@ -750,10 +769,12 @@ hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, 
     do {                                                                                            \
         if (wide)                                                                                   \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr);      \
+                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr,      \
+                               nullptr, 0, nullptr);                                              \
         else                                                                                        \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 1>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr);      \
+                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr,      \
+                               nullptr, 0, nullptr);                                              \
     } while (0)
     if (k <= 8) IMGREC_LAUNCH_MERGE(8);
     else if (k <= 10) IMGREC_LAUNCH_MERGE(10);
@@ -960,7 +981,52 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
     // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is
     // covered by the floor), the output takes kout rounds of the wave argmin
     hipLaunchKernelGGL((knn_merge_kernel<16, 1>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
-                       cd, ci, nq, nlists, kin, stride_q, stride_l, stride_l, kout, 1, 0, D, I, floor);
+                       cd, ci, nq, nlists, kin, stride_q, stride_l, stride_l, kout, 1, 0, D, I, floor,
+                       nullptr, 0, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_dyn(const float* cd, const int64_t* ci, const int* dyn, int lists_per_split,
+                            int kin, int64_t cap_q, int k, int metric, const int* out_rows,
+                            float* D, int64_t* I, hipStream_t st) {
+    if (cap_q <= 0) return hipSuccess;
+    // four waves per query: the plan can give one query block all the row splits
+    const dim3 grid((unsigned)cap_q), block(256);
+#define IMGREC_MERGE_DYN(KMV)                                                                      \
+    hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, cap_q, 0, kin,      \
+                       (int64_t)0, (int64_t)kin, (int64_t)kin, k, metric, 0, D, I, nullptr, dyn,   \
+                       lists_per_split, out_rows)
+    if (k <= 8) IMGREC_MERGE_DYN(8);
+    else if (k <= 10) IMGREC_MERGE_DYN(10);
+    else if (k <= 16) IMGREC_MERGE_DYN(16);
+    else if (k <= 32) IMGREC_MERGE_DYN(32);
+    else return hipErrorInvalidValue;
+#undef IMGREC_MERGE_DYN
+    return hipGetLastError();
+}
+
+__global__ void iota64_kernel(int64_t* __restrict__ dst, int64_t n, int64_t start) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = start + i;
+}
+
+__global__ void map_labels_kernel(int64_t* __restrict__ I, int64_t n, const int64_t* __restrict__ lmap,
+                                  int64_t offset) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && I[i] >= 0) I[i] = lmap[I[i]] + offset;
+}
+
+hipError_t launch_iota64(int64_t* dst, int64_t n, int64_t start, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(iota64_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dst, n, start);
+    return hipGetLastError();
+}
+
+hipError_t launch_map_labels(int64_t* I, int64_t n, const int64_t* lmap, int64_t offset,
+                             hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(map_labels_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, I, n,
+                       lmap, offset);
     return hipGetLastError();
 }
 

@@ -1,0 +1,130 @@
+// knn_plan.cpp — launch geometry of the fused distance + top-k kernels and the relative
+// error-bound coefficients of the candidate paths' certificate (DESIGN.md "Launch plan",
+// "bf16 path", "Split path").
+#include <cmath>
+
+#include "knn_index.h"
+
+namespace imgrec {
+
+// Fused-kernel geometry for one query chunk of the exact fp32 path.
+Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
+    Plan p{};
+    p.km = k <= 8 ? 8 : (k <= 10 ? 10 : (k <= 16 ? 16 : 32));
+    int wg_per_cu;
+    if (nq <= 32) { p.wr = 2; p.wq = 1; wg_per_cu = 3; }
+    else if (nq <= 128) { p.wr = 2; p.wq = 2; wg_per_cu = 2; }
+    // Two independent 4-wave workgroups per CU: their barriers do not line up, so one
+    // workgroup's stage bubble is filled by the other's MFMAs (31.4 vs 32.2 ms for one 8-wave
+    // (1,8) workgroup, bench config).
+    else { p.wr = 1; p.wq = 4; wg_per_cu = 2; }
+    p.bm = p.wr * 128;
+    p.bq = p.wq * 32;
+    p.nqb = (int)((nq + p.bq - 1) / p.bq);
+    p.nq_pad = p.nqb * p.bq;
+    p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+    const int target = cus * wg_per_cu;
+    int ns = (target + p.nqb - 1) / p.nqb;
+    ns = std::max(1, std::min(ns, p.ntiles));
+    p.nsplit = ns;
+    p.ncand = ns * p.wr * 2 * p.km;
+    p.wgs = p.nqb * p.nsplit;
+    return p;
+}
+
+int fallback_km(int k) { return k <= 8 ? 8 : (k <= 10 ? 10 : (k <= 16 ? 16 : 32)); }
+
+// Three (2,1) workgroups per CU (make_plan's geometry for <= 32 queries), and never fewer than
+// one per 32-query block of a full chunk, so every block of the device plan gets a workgroup.
+int fallback_grid(int cus, int64_t chunk_q) {
+    return (int)std::max<int64_t>(3 * (int64_t)cus, (chunk_q + 31) / 32);
+}
+
+// Split-path geometry: one tile shape for every batch size ((1,4) workgroups, two per CU,
+// kSplitWB row blocks per wave).
+Plan make_split_plan(int64_t ntotal, int64_t nq, int kc, int cus) {
+    Plan p{};
+    p.km = kc;
+    p.wr = 1;
+    p.wq = 4;
+    p.bm = p.wr * 32 * kSplitWB;
+    p.bq = p.wq * 32;
+    p.nqb = (int)((nq + p.bq - 1) / p.bq);
+    p.nq_pad = p.nqb * p.bq;
+    p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+    const int target = cus * 2;
+    p.nsplit = std::max(1, std::min((target + p.nqb - 1) / p.nqb, p.ntiles));
+    p.ncand = p.nsplit * p.wr * 2 * p.km;
+    p.wgs = p.nqb * p.nsplit;
+    return p;
+}
+
+// Split-bf16 candidate path (knn_refine.hip): used for batches the (1,4) plan covers, k <= 16,
+// rows padded to 32 floats.  K' = candidates kept per query for the exact rerank.
+int split_kc(int k) { return k <= 10 ? 16 : (k <= 16 ? 32 : 0); }
+
+// Relative error-bound coefficients of the certificate (DESIGN.md "Split path"), multiplied by
+// |q| * max|x| in the kernel:
+//   split dot:  3.1 * 2^-16 (dropped lo.lo / residual terms of x = hi + lo + r, |r| <= 2^-16 |x|)
+//               + 1.02 * gamma_n, n = 3 MFMAs x (dp/16) steps x 5 (a 16-term tree inside each),
+//               with unit roundoff 2^-23 (allows truncating accumulation);
+//   rerank dot: 1.02 * gamma_n, n = 4*ceil(dp/256) + 8 fp32 FMAs + butterfly levels, u = 2^-24.
+float split_coef(int dp) {
+    return (float)(3.1 * std::ldexp(1.0, -16) + 1.02 * (15.0 * (dp / 16) + 16.0) * std::ldexp(1.0, -23));
+}
+float rerank_coef(int dp) {
+    return (float)(1.02 * (4.0 * ((dp + 255) / 256) + 8.0) * std::ldexp(1.0, -24));
+}
+
+// bf16 candidate pass (one bf16 MFMA per product): the products of two bf16 values are exact in
+// fp32, so the only arithmetic error besides the operand rounding (bounded in the rerank kernel
+// from the stored residual norms) is the fp32 accumulation: 1.02 * gamma_n, n = (dpb/16) MFMAs x 5
+// (a 16-term tree inside each) + 16, with unit roundoff 2^-23 (allows truncating accumulation),
+// relative to |qh| |xh|.
+float b16_acc_coef(int dpb) {
+    return (float)(1.02 * (5.0 * (dpb / 16) + 16.0) * std::ldexp(1.0, -23));
+}
+// per-lane list length of the generic bf16 tile (the merge floor covers what a lane list drops)
+int b16_km(int k) { return k <= 16 ? 16 : 32; }
+
+constexpr int kB16NarrowQ = 32;   // batches up to this use the 32-query tile
+
+// bf16-path geometry: large batches with k <= 10 on the 256 x 256-tile kernel (one workgroup
+// per CU, lane lists of 8 / 10); otherwise (kB16WR, kB16WQ) workgroups, kB16WGPCU per CU.
+Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus, int dpb) {
+    Plan p{};
+    // (dpb bound: the 256 x 256 kernel's 32-bit lane offsets, see launch_b16_big)
+    if (nq >= kB16BigMinQ && k <= 10 && dpb <= 16384) {
+        p.big = true;
+        p.km = k <= 8 ? 8 : 10;
+        p.wr = 2;
+        p.wq = 4;
+        p.bm = kB16BigRows;
+        p.bq = kB16BigQueries;
+        p.nqb = (int)((nq + p.bq - 1) / p.bq);
+        p.nq_pad = p.nqb * p.bq;
+        p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+        p.nsplit = std::max(1, std::min((cus + p.nqb - 1) / p.nqb, p.ntiles));
+        p.ncand = p.nsplit * p.km;               // lists folded to one per (query, split)
+        p.wgs = p.nqb * p.nsplit;
+        return p;
+    }
+    p.km = b16_km(k);
+    // batches of <= 32 queries: a 32-query tile (the (1,4) tile would pad them to 128 and spend
+    // four times the matrix work of an HBM-bound search)
+    const bool narrow = nq <= kB16NarrowQ;
+    p.wr = narrow ? 2 : kB16WR;
+    p.wq = narrow ? 1 : kB16WQ;
+    p.bm = p.wr * 32 * kB16WB;
+    p.bq = p.wq * 32;
+    p.nqb = (int)((nq + p.bq - 1) / p.bq);
+    p.nq_pad = p.nqb * p.bq;
+    p.ntiles = (int)((ntotal + p.bm - 1) / p.bm);
+    const int target = cus * kB16WGPCU;
+    p.nsplit = std::max(1, std::min((target + p.nqb - 1) / p.nqb, p.ntiles));
+    p.ncand = p.nsplit * p.wr * 2 * p.km;
+    p.wgs = p.nqb * p.nsplit;
+    return p;
+}
+
+}  // namespace imgrec

@@ -27,6 +27,7 @@
 #include <algorithm>
 
 #include "knn_kernels.h"
+#include "wave_ops.h"
 
 namespace imgrec {
 
@@ -190,36 +191,41 @@ __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
     return d1 < d2 || (d1 == d2 && i1 < i2);
 }
 
-// One workgroup of kRerankWaves waves per query.  cd/ci: the merged approximate candidates,
+// One workgroup of kRerankWaves waves per query.  a.cd/a.ci: the merged approximate candidates,
 // nq x kc, ascending raw keys (L2 distance or -ip), empty = label -1.
 // IT > 0: the query row sits in registers (IT float4 per lane, dp <= 256 IT) and every wave loads
 // its candidates' rows kRerankRows at a time, all loads in flight at once; IT = 0 streams the
 // query with the rows (any dp).
-constexpr int kRerankWaves = 8, kRerankRows = 2;
+//
+// A query whose certificate fails gets a second chance in the same workgroup (a.raw_d != NULL):
+// every entry of the candidate pass's per-split lists (not only the merged K' = 64) that can
+// still rank in the top k is reranked, and the certificate is re-run with the list floor alone
+// (the smallest last key of a full list: every row outside all lists is at least that).  Only if
+// that fails too is the query listed for the exact fp32 re-run (run_fallback, on device).
+constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
 template <int IT>
 __global__ void __launch_bounds__(kRerankWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
-rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qnorm, int dp,
-                      const float* __restrict__ xb, const float* __restrict__ xn,
-                      const float* __restrict__ xn_max, int64_t id_offset,
-                      const float* __restrict__ cd, const int64_t* __restrict__ ci, int kc,
-                      int64_t nq, int k, int metric, float c_split, float c_fp,
-                      float* __restrict__ D, int64_t* __restrict__ I, int* __restrict__ fail_count,
-                      int* __restrict__ fail_list, float* __restrict__ err_ratio, int mode,
-                      const float* __restrict__ q_resid, const float* __restrict__ xr_max,
-                      const float* __restrict__ floor) {
+rerank_certify_kernel(const RerankArgs a) {
     __shared__ float skey[64];
     __shared__ int64_t slab[64];
+    __shared__ int s_fail;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int64_t q = blockIdx.x;
-    const float* qv = qp + q * dp;
-    const float qn = qnorm[q];
+    const int dp = a.dp, kc = a.kc, k = a.k, metric = a.metric;
+    const int64_t id_offset = a.id_offset;
+    const float* __restrict__ cd = a.cd;
+    const int64_t* __restrict__ ci = a.ci;
+    const float* __restrict__ xb = a.xb;
+    const float* __restrict__ xn = a.xn;
+    const float* qv = a.qp + q * dp;
+    const float qn = a.qnorm[q];
     const int64_t lab = lane < kc ? ci[q * kc + lane] : (int64_t)-1;
     const float ak = lane < kc ? cd[q * kc + lane] : INFINITY;   // approximate key, ascending
     const bool valid = lab >= 0;
     const int nvalid = __popcll(__ballot(valid));               // valid candidates come first
 
-    const float xm = *xn_max;
+    const float xm = *a.xn_max;
     const float nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
     const float u = 1.0f / 8388608.f;               // 2^-23
     // |approximate q.x - q.x| for every row:
@@ -228,12 +234,13 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
     //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max |x|,
     //          |qh| <= |q| + dq, |xh| <= X + R), inflated for the fp32 evaluation of the bound
     float e_ip;
-    if (mode == kModeBF16) {
-        const float sq = sqrtf(qn), X = sqrtf(xm), R = *xr_max, dq = q_resid[q];
-        e_ip = (sq * R + dq * (X + R) + c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
+    if (a.mode == kModeBF16) {
+        const float sq = sqrtf(qn), X = sqrtf(xm), R = *a.xr_max, dq = a.q_resid[q];
+        e_ip = (sq * R + dq * (X + R) + a.c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
     } else {
-        e_ip = c_split * nn;
+        e_ip = a.c_split * nn;
     }
+    const float c_fp = a.c_fp;
     auto bound_a = [&](float v) {                   // |approx key - exact key| bound at key v
         return metric == 1 ? 2.f * e_ip + 2.f * u * (qn + xm + fabsf(v)) : e_ip;
     };
@@ -246,54 +253,30 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
     // a_k + 2 (E_a + E_f) cannot rank before them.  The prefix P = {approx <= that} is reranked;
     // the first candidate left out bounds every excluded candidate's approximate key from below.
     int m = nvalid;
+    float thr = INFINITY;
     if (nvalid >= k) {
         const float a_k = __shfl(ak, k - 1, 64);
-        const float thr = a_k + 2.02f * (bound_a(a_k) + bound_f(a_k));
+        thr = a_k + 2.02f * (bound_a(a_k) + bound_f(a_k));
         m = __popcll(__ballot(valid && ak <= thr));
     }
 
-    // exact fp32 keys of the prefix: candidate c goes to wave c % kRerankWaves (each candidate's
-    // sum has the same order wherever it runs)
+    // exact fp32 dot products, kRerankRows rows per wave at a time; a row's sum has the same
+    // order wherever and in whichever pass it runs, so its key is the same bits
     const int n4 = dp / 4;
     const float4* q4 = reinterpret_cast<const float4*>(qv);
-    auto row_of = [&](int c) {
-        const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
-        const int hi32 = __shfl((int)(lab >> 32), c, 64);
-        const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
-        return reinterpret_cast<const float4*>(xb + (l - id_offset) * dp);
-    };
-    auto finish = [&](float (&acc)[kRerankRows], int c0) {
-#pragma unroll
-        for (int v = 0; v < kRerankRows; ++v) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
-            const int c = c0 + kRerankWaves * v;
-            if (lane != c || c >= m) continue;                   // candidate c sits in lane c
-            float kv;
-            if (metric == 1) {
-                kv = fmaf(-2.f, acc[v], qn + xn[lab - id_offset]);
-                kv = kv < 0.f ? 0.f : kv;
-            } else {
-                kv = -acc[v];
-            }
-            skey[c] = kv;
-        }
-    };
+    float4 qr[IT > 0 ? IT : 1];
     if constexpr (IT > 0) {
-        float4 qr[IT];
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int i = lane + 64 * it;
             qr[it] = i < n4 ? q4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
-            const float4* r4[kRerankRows];
-            float acc[kRerankRows];
+    }
+    auto dots = [&](const float4* const (&r4)[kRerankRows], float (&acc)[kRerankRows])
+        __attribute__((always_inline)) {
 #pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
-                r4[v] = row_of(min(c0 + kRerankWaves * v, m - 1));   // clamped: loads unconditional
-                acc[v] = 0.f;
-            }
+        for (int v = 0; v < kRerankRows; ++v) acc[v] = 0.f;
+        if constexpr (IT > 0) {
             float4 b[kRerankRows][IT];
 #pragma unroll
             for (int v = 0; v < kRerankRows; ++v)
@@ -311,91 +294,231 @@ rerank_certify_kernel(const float* __restrict__ qp, const float* __restrict__ qn
                     acc[v] = fmaf(qr[it].z, b[v][it].z, acc[v]);
                     acc[v] = fmaf(qr[it].w, b[v][it].w, acc[v]);
                 }
-            finish(acc, c0);
-        }
-    } else {
-        for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
-            const float4* r4[kRerankRows];
-            float acc[kRerankRows];
-#pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
-                r4[v] = row_of(min(c0 + kRerankWaves * v, m - 1));
-                acc[v] = 0.f;
-            }
+        } else {
 #pragma unroll 4
             for (int i = lane; i < n4; i += 64) {
-                const float4 a = q4[i];
+                const float4 qa = q4[i];
 #pragma unroll
                 for (int v = 0; v < kRerankRows; ++v) {
                     const float4 bb = r4[v][i];
-                    acc[v] = fmaf(a.x, bb.x, acc[v]);
-                    acc[v] = fmaf(a.y, bb.y, acc[v]);
-                    acc[v] = fmaf(a.z, bb.z, acc[v]);
-                    acc[v] = fmaf(a.w, bb.w, acc[v]);
+                    acc[v] = fmaf(qa.x, bb.x, acc[v]);
+                    acc[v] = fmaf(qa.y, bb.y, acc[v]);
+                    acc[v] = fmaf(qa.z, bb.z, acc[v]);
+                    acc[v] = fmaf(qa.w, bb.w, acc[v]);
                 }
             }
-            finish(acc, c0);
+        }
+#pragma unroll
+        for (int v = 0; v < kRerankRows; ++v)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
+    };
+    auto key_of = [&](float ip, int64_t l) __attribute__((always_inline)) {
+        if (metric == 1) {
+            const float kv = fmaf(-2.f, ip, qn + xn[l - id_offset]);
+            return kv < 0.f ? 0.f : kv;
+        }
+        return -ip;
+    };
+    auto row_ptr = [&](int64_t l) __attribute__((always_inline)) {
+        return reinterpret_cast<const float4*>(xb + (l - id_offset) * dp);
+    };
+    auto lane_label = [&](int c) __attribute__((always_inline)) {
+        const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
+        const int hi32 = __shfl((int)(lab >> 32), c, 64);
+        return ((int64_t)hi32 << 32) | (uint32_t)lo32;
+    };
+    // the prefix: candidate c goes to wave c % kRerankWaves, sits in lane c
+    for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
+        const float4* r4[kRerankRows];
+        float acc[kRerankRows];
+#pragma unroll
+        for (int v = 0; v < kRerankRows; ++v)      // clamped: loads unconditional
+            r4[v] = row_ptr(lane_label(min(c0 + kRerankWaves * v, m - 1)));
+        dots(r4, acc);
+#pragma unroll
+        for (int v = 0; v < kRerankRows; ++v) {
+            const int c = c0 + kRerankWaves * v;
+            if (lane == c && c < m) skey[c] = key_of(acc[v], lab);
         }
     }
-    if (wave == 0 && lane < 64) slab[lane] = lab;
+    if (wave == 0) slab[lane] = lab;
     __syncthreads();
-    if (wave != 0) return;
-    const float key = lane < m ? skey[lane] : INFINITY;
 
-    // rank of this lane's candidate inside the prefix by (key, label)
-    const bool inP = lane < m;
-    int rank = 0;
-    for (int i = 0; i < m; ++i)
-        if (inP && ranks_before_r(skey[i], slab[i], key, lab)) ++rank;
-    if (inP && rank < k) {
-        D[q * k + rank] = (metric == 1) ? key : -key;
-        I[q * k + rank] = lab;
-    }
-    if (lane >= m && lane < k) {
-        D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
-        I[q * k + lane] = -1;
-    }
-
-    // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
-    // whenever the bounds hold; reported by knn_search_stats so tests and the bench can watch it)
-    if (inP) {
-        const float r = fabsf(ak - key) / (bound_a(ak) + bound_f(key));
-        atomicMax(reinterpret_cast<unsigned*>(err_ratio), __float_as_uint(r));
-    }
-
-    // certificate: tau = smallest approximate key a row outside the prefix can have — the K'-th
-    // candidate's (when the set is full), the merge floor (rows dropped by full lists) and the
-    // first candidate left out of the prefix; +inf means every row was reranked
-    const int64_t lab_tau = ci[q * kc + kc - 1];
-    float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
-    if (floor) tau = fminf(tau, floor[q]);
-    const float a_out = __shfl(ak, min(m, 63), 64);
-    if (m < nvalid) tau = fminf(tau, a_out);
-    bool failed = false;                            // tau = +inf: every row was reranked
-    if (tau != INFINITY) {
-        float sk = (inP && rank == k - 1) ? key : -INFINITY;
+    if (wave == 0) {
+        const float key = lane < m ? skey[lane] : INFINITY;
+        // rank of this lane's candidate inside the prefix by (key, label)
+        const bool inP = lane < m;
+        int rank = 0;
+        for (int i = 0; i < m; ++i)
+            if (inP && ranks_before_r(skey[i], slab[i], key, lab)) ++rank;
+        if (inP && rank < k) {
+            a.D[q * k + rank] = (metric == 1) ? key : -key;
+            a.I[q * k + rank] = lab;
+        }
+        if (lane >= m && lane < k) {
+            a.D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
+            a.I[q * k + lane] = -1;
+        }
+        // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
+        // whenever the bounds hold; reported by knn_search_stats so tests and the bench watch it)
+        if (inP) {
+            const float r = fabsf(ak - key) / (bound_a(ak) + bound_f(key));
+            atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+        }
+        // certificate: tau = smallest approximate key a row outside the prefix can have — the
+        // K'-th candidate's (when the set is full), the merge floor (rows dropped by full lists)
+        // and the first candidate left out of the prefix; +inf means every row was reranked
+        const int64_t lab_tau = ci[q * kc + kc - 1];
+        float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
+        if (a.floor) tau = fminf(tau, a.floor[q]);
+        const float a_out = __shfl(ak, min(m, 63), 64);
+        if (m < nvalid) tau = fminf(tau, a_out);
+        bool failed = false;                        // tau = +inf: every row was reranked
+        if (tau != INFINITY) {
+            float sk = (inP && rank == k - 1) ? key : -INFINITY;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
-        // fewer than k reranked rows while rows were left out: nothing to certify with
-        failed = !(m >= k && (tau - bound_a(tau)) > (sk + bound_f(sk)));
+            for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
+            // fewer than k reranked rows while rows were left out: nothing to certify with
+            failed = !(m >= k && (tau - bound_a(tau)) > (sk + bound_f(sk)));
+        }
+        if (lane == 0) s_fail = failed ? 1 : 0;
     }
-    if (failed && lane == 0) fail_list[atomicAdd(fail_count, 1)] = (int)q;
+    __syncthreads();
+    if (!s_fail) return;
+    if (!a.raw_d) {
+        if (threadIdx.x == 0) {
+            atomicAdd(a.stats + 2, 1);
+            a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
+        }
+        return;
+    }
+
+    // ---- second chance: every per-split list entry with approximate key <= thr (those above it
+    // cannot reach the top k, by the prefix argument), certified against the list floor --------
+    __shared__ float w_key[kWideCap], w_apx[kWideCap];
+    __shared__ int64_t w_lab[kWideCap];
+    __shared__ float o_key[64];
+    __shared__ int64_t o_lab[64];
+    __shared__ int w_n;
+    __shared__ unsigned w_tau;
+    __shared__ float s_sk;
+    constexpr int NT = kRerankWaves * 64;
+    const int t = threadIdx.x;
+    if (t == 0) {
+        w_n = 0;
+        w_tau = key_bits_ordered(INFINITY);
+        s_sk = -INFINITY;
+        atomicAdd(a.stats + 2, 1);
+    }
+    if (t < 64) o_lab[t] = -1;
+    __syncthreads();
+    const float* rd = a.raw_d + q * a.raw_stride_q;
+    const int64_t* ri = a.raw_i + q * a.raw_stride_q;
+    const int km = a.raw_km, ne = a.raw_lists * km;
+    for (int l = t; l < a.raw_lists; l += NT) {
+        const int e = l * km + km - 1;
+        if (ri[e] >= 0) atomicMin(&w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
+    }
+    for (int e = t; e < ne; e += NT) {
+        const int64_t l = ri[e];
+        const float v = rd[e];
+        if (l >= 0 && v <= thr) {
+            const int s = atomicAdd(&w_n, 1);
+            if (s < kWideCap) { w_apx[s] = v; w_lab[s] = l; }
+        }
+    }
+    __syncthreads();
+    const int n = w_n;
+    bool ok = n <= kWideCap;
+    if (ok) {
+        for (int c0 = wave; c0 < n; c0 += kRerankWaves * kRerankRows) {
+            const float4* r4[kRerankRows];
+            float acc[kRerankRows];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) r4[v] = row_ptr(w_lab[min(c0 + kRerankWaves * v, n - 1)]);
+            dots(r4, acc);
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                const int c = c0 + kRerankWaves * v;
+                if (lane == 0 && c < n) w_key[c] = key_of(acc[v], w_lab[c]);
+            }
+        }
+        __syncthreads();
+        // rank of every reranked entry by (key, label): labels are distinct (a row sits in one list)
+        for (int s = t; s < n; s += NT) {
+            const float kv = w_key[s];
+            const int64_t lb = w_lab[s];
+            int rank = 0;
+            for (int j = 0; j < n && rank < k; ++j) rank += ranks_before_r(w_key[j], w_lab[j], kv, lb) ? 1 : 0;
+            if (rank < k) {
+                o_key[rank] = kv;
+                o_lab[rank] = lb;
+                if (rank == k - 1) s_sk = kv;
+            }
+            const float r = fabsf(w_apx[s] - kv) / (bound_a(w_apx[s]) + bound_f(kv));
+            atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+        }
+        __syncthreads();
+        // every row outside the lists has approximate key >= the floor (+inf: no list dropped a
+        // row, so every row of the corpus was a candidate and W holds all that can matter)
+        const float tauL = key_from_ordered(w_tau);
+        ok = tauL == INFINITY || (tauL - bound_a(tauL)) > (s_sk + bound_f(s_sk));
+    }
+    if (ok) {
+        if (t < k) {
+            const int64_t lb = o_lab[t];
+            a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
+                                    : ((metric == 1) ? o_key[t] : -o_key[t]);
+            a.I[q * k + t] = lb;
+        }
+    } else if (t == 0) {
+        a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
+    }
 }
 
-// After a rerank (the kernel boundary orders every workgroup's stats atomics before it): publish
-// the uncertified count and the error ratio to the host mailbox (pinned, mapped; the host spins
-// on mail[0] == seq instead of a device-to-host copy and a stream synchronisation) and zero the
-// counters for the next search.  One lane; vector stores only.
-__global__ void __launch_bounds__(64)
-publish_stats_kernel(int* __restrict__ fail_count, int* __restrict__ err_bits, int* __restrict__ mail,
-                     int seq) {
-    if (threadIdx.x != 0) return;
-    const int nf = *fail_count, er = *err_bits;
-    *fail_count = 0;
-    *err_bits = 0;
-    __hip_atomic_store(mail + 1, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(mail + 2, er, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(mail, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// Device-side exact re-run of the queries the certificate could not settle (no host round trip):
+// reads the uncertified count of this chunk (stats parity p), gathers those queries' padded rows
+// and norms (zero rows up to the next multiple of 32) and writes the launch plan the fused exact
+// kernel and the merge read from device memory: dyn = {count, query blocks, row splits, list
+// entries per query}.  Block 0 also folds this chunk's stats into the per-search accumulators and
+// zeroes the other parity for the next chunk (its previous user finished: stream order).
+__global__ void __launch_bounds__(256)
+fallback_prep_kernel(int* __restrict__ stat, int parity, int first, const int* __restrict__ list,
+                     const float* __restrict__ qpad, const float* __restrict__ qnorm, int dp,
+                     int grid_wgs, int ntiles, int lists_km, float* __restrict__ fq,
+                     float* __restrict__ fqn, int* __restrict__ dyn) {
+    const int* sp = stat + 4 * parity;
+    const int count = sp[0];
+    const int nqb = (count + 31) / 32;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int nsplit = nqb ? max(1, min(grid_wgs / nqb, ntiles)) : 0;
+        dyn[0] = count;
+        dyn[1] = nqb;
+        dyn[2] = nsplit;
+        dyn[3] = nsplit * lists_km;
+        int* acc = stat + 8;
+        acc[0] = first ? sp[0] : acc[0] + sp[0];
+        acc[1] = first ? sp[1] : max(acc[1], sp[1]);        // ratio >= 0: bit order = float order
+        acc[2] = first ? sp[2] : acc[2] + sp[2];
+        int* other = stat + 4 * (parity ^ 1);
+        other[0] = 0; other[1] = 0; other[2] = 0;
+    }
+    const int lane = threadIdx.x & 63;
+    const int64_t rows = (int64_t)nqb * 32;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
+         row += (int64_t)gridDim.x * 4) {
+        float* o = fq + row * dp;
+        if (row >= count) {
+            for (int j = lane; j < dp; j += 64) o[j] = 0.f;
+            if (lane == 0) fqn[row] = 0.f;
+            continue;
+        }
+        const int src = list[row];
+        const float* s = qpad + (int64_t)src * dp;
+        for (int j = lane; j < dp; j += 64) o[j] = s[j];
+        if (lane == 0) fqn[row] = qnorm[src];
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -452,21 +575,26 @@ hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32
 
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
-    if (a.kc > 64 || a.k > a.kc || a.dp % 4 != 0 || !a.mail) return hipErrorInvalidValue;
+    if (a.kc > 64 || a.k > a.kc || a.k > 64 || a.dp % 4 != 0 || !a.stats || !a.fail_list)
+        return hipErrorInvalidValue;
+    if (a.raw_d && (!a.raw_i || a.raw_km < a.k || a.raw_lists <= 0)) return hipErrorInvalidValue;
 #define IMGREC_RERANK(ITV)                                                                          \
     hipLaunchKernelGGL((rerank_certify_kernel<ITV>), dim3((unsigned)a.nq), dim3(kRerankWaves * 64), \
-                       0, st, a.qp, a.qnorm, a.dp, a.xb, a.xn, a.xn_max, a.id_offset, a.cd, a.ci,   \
-                       a.kc, a.nq, a.k, a.metric, a.c_split, a.c_fp, a.D, a.I, a.fail_count,        \
-                       a.fail_list, a.err_ratio, a.mode, a.q_resid, a.xr_max, a.floor)
+                       0, st, a)
     if (a.dp <= 512) IMGREC_RERANK(2);
     else if (a.dp <= 1024) IMGREC_RERANK(4);
     else if (a.dp <= 2048) IMGREC_RERANK(8);
     else IMGREC_RERANK(0);
 #undef IMGREC_RERANK
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(publish_stats_kernel, dim3(1), dim3(64), 0, st, a.fail_count,
-                       reinterpret_cast<int*>(a.err_ratio), a.mail, a.seq);
+    return hipGetLastError();
+}
+
+hipError_t launch_fallback_prep(int* stat, int parity, int first, const int* list, const float* qpad,
+                                const float* qnorm, int dp, int grid_wgs, int ntiles, int lists_km,
+                                int64_t cap_rows, float* fq, float* fqn, int* dyn, hipStream_t st) {
+    const int64_t blocks = std::min<int64_t>(256, std::max<int64_t>(1, (cap_rows + 3) / 4));
+    hipLaunchKernelGGL(fallback_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, stat, parity,
+                       first, list, qpad, qnorm, dp, grid_wgs, ntiles, lists_km, fq, fqn, dyn);
     return hipGetLastError();
 }
 

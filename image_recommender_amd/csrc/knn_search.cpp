@@ -1,0 +1,323 @@
+// knn_search.cpp — the three search arithmetics of one k-NN index and their device-side
+// certificate handling (DESIGN.md "Kernels"):
+//
+//   exact   the fused fp32 MFMA distance + top-k kernel, then the list merge;
+//   bf16    bf16 candidate pass (one bf16 MFMA per product) -> candidate merge (top K' = 64 +
+//           list floor) -> fp32 rerank + certificate, with a second chance over every per-split
+//           list entry for queries the first certificate cannot settle;
+//   split   split-bf16 candidate pass (three bf16 MFMAs per product) -> merge -> rerank +
+//           certificate (+ second chance).
+//
+// Queries no certificate settles are re-run exactly by a device-planned launch of the fused fp32
+// kernel (run_fallback): the count never travels to the host, so knn_search_device enqueues a
+// whole search without waiting for the GPU.
+#include <cstring>
+
+#include "knn_index.h"
+
+namespace imgrec {
+
+namespace {
+
+// Timing events around the dominant (fused) kernel launch of a chunk.
+int timed_begin(knn_index* ix, hipStream_t st, hipEvent_t* e1) {
+    *e1 = nullptr;
+    if (!ix->timing) return KNN_OK;
+    if (ix->ev_used + 2 > ix->ev.size()) {
+        for (int i = 0; i < 64; ++i) {
+            hipEvent_t e;
+            KNN_HIP(hipEventCreate(&e));
+            ix->ev.push_back(e);
+        }
+    }
+    KNN_HIP(hipEventRecord(ix->ev[ix->ev_used], st));
+    *e1 = ix->ev[ix->ev_used + 1];
+    ix->ev_used += 2;
+    return KNN_OK;
+}
+
+// Exact fp32 path over nq padded queries (qpad holds make_plan(nq).nq_pad zero-padded rows).
+int exact_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+                int64_t* I, hipStream_t st, bool timed) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const Plan p = make_plan(ix->ntotal, nq, k, ix->cus);
+    int rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    TileArgs a{};
+    a.wr = p.wr; a.wq = p.wq; a.km = p.km;
+    a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
+    a.qp = qpad; a.qnorm = qnorm; a.nq = (int)nq; a.metric = kmetric;
+    a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
+    a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.mode = kModeF32;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(launch_tile_topk(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    KNN_HIP(launch_merge(ix->cand_d, ix->cand_i, nq, p.ncand / p.km, p.km, p.ncand, p.km, k,
+                         kmetric, 0, D, I, st));
+    return KNN_OK;
+}
+
+// max |x|^2 (and max bf16 residual) over the stored rows, recomputed after rows change
+int refresh_maxima(knn_index* ix, hipStream_t st) {
+    if (!ix->xn_max_stale) return KNN_OK;
+    int rc;
+    if ((rc = grow(&ix->xn_max, &ix->xn_max_cap, 1)) != KNN_OK) return rc;
+    KNN_HIP(launch_max_norm(ix->xn, ix->ntotal, ix->xn_max, st));
+    if (ix->b16_ok) {
+        if ((rc = grow(&ix->xr_max, &ix->xr_max_cap, 1)) != KNN_OK) return rc;
+        KNN_HIP(launch_max_norm(ix->xr, ix->ntotal, ix->xr_max, st));
+    }
+    ix->xn_max_stale = false;
+    return KNN_OK;
+}
+
+// Certificate counters (two chunk parities + per-search totals, zeroed once here; the fallback
+// prep kernel folds and re-zeroes them) and the uncertified-query list.
+int grow_stats(knn_index* ix, int64_t nq, hipStream_t st) {
+    if (!ix->stat) {
+        KNN_HIP(hipMalloc((void**)&ix->stat, 12 * sizeof(int)));
+        KNN_HIP(hipMemsetAsync(ix->stat, 0, 12 * sizeof(int), st));
+        ix->stat_seq = 0;
+    }
+    return grow(&ix->fail, &ix->fail_cap, (size_t)nq);
+}
+
+// Exact fp32 re-run of the queries this chunk's certificate left (list ix->fail, count in the
+// stats parity), planned on device: a fixed grid of (2,1) exact-kernel workgroups, those beyond
+// the plan exiting at once, then a merge that scatters each result row into place.  With nothing
+// to re-run it costs three near-empty launches.
+int run_fallback(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+                 int64_t* I, hipStream_t st, int parity, bool first) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const int km = fallback_km(k);
+    const int grid = fallback_grid(ix->cus, nq);
+    const int64_t cap_rows = round_up(nq, 32);
+    const int bm = 128 * kFallbackWR;
+    const int ntiles = (int)((ix->ntotal + bm - 1) / bm);
+    const int lists_km = 2 * kFallbackWR * km;
+    // candidate lists: at most `grid` (query block, row split) pairs of 32 queries each
+    const size_t ncap = (size_t)grid * 32 * lists_km;
+    int rc;
+    if ((rc = grow(&ix->fb_q, &ix->fb_q_cap, (size_t)cap_rows * ix->dp)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fb_qn, &ix->fb_qn_cap, (size_t)cap_rows)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fb_cd, &ix->fb_cd_cap, ncap)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->fb_ci, &ix->fb_ci_cap, ncap)) != KNN_OK) return rc;
+    if (!ix->fb_dyn) KNN_HIP(hipMalloc((void**)&ix->fb_dyn, 4 * sizeof(int)));
+    KNN_HIP(launch_fallback_prep(ix->stat, parity, first ? 1 : 0, ix->fail, qpad, qnorm, ix->dp,
+                                 grid, ntiles, lists_km, cap_rows, ix->fb_q, ix->fb_qn, ix->fb_dyn,
+                                 st));
+    TileArgs a{};
+    a.wr = kFallbackWR; a.wq = 1; a.km = km; a.mode = kModeF32;
+    a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
+    a.qp = ix->fb_q; a.qnorm = ix->fb_qn; a.nq = 0; a.metric = kmetric;
+    a.ntiles = ntiles; a.nsplit = 0; a.nqb = 0; a.id_offset = ix->id_offset;
+    a.cand_d = ix->fb_cd; a.cand_i = ix->fb_ci; a.ncand = 0;
+    a.dyn = ix->fb_dyn; a.grid = grid;
+    KNN_HIP(launch_tile_topk(a, st));
+    KNN_HIP(launch_merge_dyn(ix->fb_cd, ix->fb_ci, ix->fb_dyn, 2 * kFallbackWR, km, nq, k, kmetric,
+                             ix->fail, D, I, st));
+    return KNN_OK;
+}
+
+// The rerank + certificate of a candidate chunk and the device-side exact re-run after it.
+int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* qnorm, int64_t nq,
+                  int k, float* D, int64_t* I, hipStream_t st, bool first) {
+    const int parity = ix->stat_seq & 1;
+    r.stats = ix->stat + 4 * parity;
+    r.fail_list = ix->fail;
+    KNN_HIP(launch_rerank_certify(r, st));
+    const int rc = run_fallback(ix, qpad, qnorm, nq, k, D, I, st, parity, first);
+    if (rc != KNN_OK) {           // the parities may hold this chunk's counts: start clean
+        (void)hipMemsetAsync(ix->stat, 0, 12 * sizeof(int), st);
+        ix->stat_seq = 0;
+        return rc;
+    }
+    ++ix->stat_seq;
+    ix->stat_valid = true;
+    ix->last_split_queries += nq;
+    return KNN_OK;
+}
+
+// bf16 candidates (one bf16 MFMA per product) + exact fp32 rerank of K' = 64 + certificate.
+int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+              int64_t* I, hipStream_t st, bool timed, bool q_ready, bool first) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const int kc = kB16Cand;
+    const Plan p = make_b16_plan(ix->ntotal, nq, k, ix->cus, ix->dpb);
+    const int km = p.km;
+    int rc;
+    if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)p.nq_pad * ix->dpb)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->q_resid, &ix->q_resid_cap, (size_t)p.nq_pad)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
+    if ((rc = grow_stats(ix, nq, st)) != KNN_OK) return rc;
+    if (!q_ready)   // else search_locked's fused query prep already wrote qb16 / q_resid
+        KNN_HIP(launch_bf16_rows(qpad, p.nq_pad, ix->dp, ix->dpb, ix->qb16, ix->q_resid, st));
+    TileArgs a{};
+    a.wr = p.wr; a.wq = p.wq; a.km = km; a.wb = kB16WB; a.mode = kModeBF16;
+    a.xb = reinterpret_cast<const float*>(ix->xh); a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
+    a.dp = ix->dpb / 2; a.qp = reinterpret_cast<const float*>(ix->qb16); a.qnorm = qnorm;
+    a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
+    a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(p.big ? launch_b16_big(a, st) : launch_tile_topk(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    const int nlists = p.ncand / km, ngrp = (nlists + 63) / 64;
+    if (ngrp > 1) {
+        if ((rc = grow(&ix->mws_d, &ix->mws_d_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
+    }
+    KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
+                                    ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
+                                    ix->mws_d, ix->mws_i, ix->mws_f, st));
+    RerankArgs r{};
+    r.mode = kModeBF16;
+    r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
+    r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
+    r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = b16_acc_coef(ix->dpb);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+    r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
+    r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = km;
+    r.raw_stride_q = p.ncand;
+    return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
+}
+
+// Split-bf16 candidates + exact rerank + certificate.
+int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+                int64_t* I, hipStream_t st, bool timed, bool first) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const int kc = split_kc(k);
+    const Plan p = make_split_plan(ix->ntotal, nq, kc, ix->cus);
+    int rc;
+    if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->qsplit, &ix->qsplit_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow_stats(ix, nq, st)) != KNN_OK) return rc;
+    KNN_HIP(launch_split_rows(qpad, p.nq_pad, ix->dp, kSplitBK, ix->qsplit, st));
+    TileArgs a{};
+    a.wr = p.wr; a.wq = p.wq; a.km = kc;
+    a.xb = reinterpret_cast<const float*>(ix->xs); a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
+    a.dp = ix->dp; a.qp = reinterpret_cast<const float*>(ix->qsplit); a.qnorm = qnorm;
+    a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
+    a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i;
+    a.ncand = p.ncand; a.mode = kModeSplit;
+    a.wb = kSplitWB; a.sbk = kSplitBK;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(launch_tile_topk(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    // global top-K' approximate candidates, raw ascending keys (merge in its L2 convention)
+    KNN_HIP(launch_merge(ix->cand_d, ix->cand_i, nq, p.ncand / kc, kc, p.ncand, kc, kc, 1, 0,
+                         ix->cand2_d, ix->cand2_i, st));
+    RerankArgs r{};
+    r.mode = kModeSplit;
+    r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
+    r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
+    r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = split_coef(ix->dp);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+    r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = p.ncand / kc; r.raw_km = kc;
+    r.raw_stride_q = p.ncand;
+    return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
+}
+
+}  // namespace
+
+// AUTO: large batches are matrix-bound (bf16 MFMA vs fp32 MFMA) once the corpus amortises the
+// rerank; small batches are HBM-bound (the bf16 copy streams half the bytes) once the corpus is
+// large enough to repay the candidate path's fixed cost (~0.1-0.2 ms).
+constexpr int64_t kB16MinRowsLarge = 16384, kB16MinRowsSmall = 131072;
+bool use_b16(const knn_index* ix, int64_t nq, int k) {
+    if (!ix->b16_ok || k > KNN_MAX_K) return false;
+    if (ix->mode == KNN_SEARCH_BF16) return true;
+    if (ix->mode != KNN_SEARCH_AUTO) return false;
+    return ix->ntotal >= (nq > 128 ? kB16MinRowsLarge : kB16MinRowsSmall);
+}
+
+bool use_split(const knn_index* ix, int64_t nq, int k) {
+    if (!ix->split_ok || ix->mode == KNN_SEARCH_EXACT || split_kc(k) == 0) return false;
+    if (ix->mode == KNN_SEARCH_SPLIT) return true;
+    // auto (when the bf16 path is unavailable): batches the (1,4) plan covers, corpora with
+    // enough rows to amortise the rerank
+    return ix->mode == KNN_SEARCH_AUTO && nq > 128 && ix->ntotal >= 16384;
+}
+
+int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
+                  hipStream_t st) {
+    const int normalize = ix->metric == KNN_METRIC_COSINE;
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    ix->last_split_queries = 0;
+    ix->stat_valid = false;
+    if (ix->ntotal == 0) {
+        KNN_HIP(launch_fill_empty(D, I, nq * (int64_t)k, kmetric, st));
+        return KNN_OK;
+    }
+    bool first_cand = true;
+    for (int64_t c0 = 0; c0 < nq; c0 += kQueryChunk) {
+        const int64_t cn = std::min(kQueryChunk, nq - c0);
+        const bool b16 = use_b16(ix, cn, k);
+        const bool split = !b16 && use_split(ix, cn, k);
+        // padding: the query tile of the plan this chunk will run (and the exact re-run's 32)
+        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
+                     : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
+                             : make_plan(ix->ntotal, cn, k, ix->cus);
+        const int64_t nq_pad = p.nq_pad;
+        int rc;
+        if (c0 == 0) ix->last_path = b16 ? 2 : (split ? 1 : 0);
+        if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;
+        bool q_ready = false;
+        if (b16 && ix->dpb <= 4096) {   // fused query prep: fp32 padded rows + norms + bf16 + residuals
+            if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)nq_pad * ix->dpb)) != KNN_OK) return rc;
+            if ((rc = grow(&ix->q_resid, &ix->q_resid_cap, (size_t)nq_pad)) != KNN_OK) return rc;
+            KNN_HIP(launch_query_prep_b16(q + c0 * ix->d, cn, ix->d, ix->dp, ix->dpb, nq_pad,
+                                          normalize, ix->qpad, ix->qnorm, ix->qb16, ix->q_resid, st));
+            q_ready = true;
+        } else {
+            KNN_HIP(launch_rows_ingest(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
+                                       ix->qpad, ix->qnorm, st));
+        }
+        float* Dc = D + c0 * k;
+        int64_t* Ic = I + c0 * k;
+        if (b16 || split) {
+            rc = b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, q_ready, first_cand)
+                     : split_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, first_cand);
+            first_cand = false;
+        } else {
+            rc = exact_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true);
+        }
+        if (rc != KNN_OK) return rc;
+    }
+    return KNN_OK;
+}
+
+// Totals of the last search's candidate chunks (waits for that search to finish).
+int read_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int64_t* first_fail,
+                      float* ratio) {
+    *split_q = ix->last_split_queries;
+    *fallback_q = 0;
+    if (first_fail) *first_fail = 0;
+    if (ratio) *ratio = 0.f;
+    if (!ix->stat_valid) return KNN_OK;
+    int rc;
+    if ((rc = fence_begin(ix, ix->stream)) != KNN_OK) return rc;
+    int acc[3] = {0, 0, 0};
+    KNN_HIP(hipMemcpyAsync(acc, ix->stat + 8, sizeof(acc), hipMemcpyDeviceToHost, ix->stream));
+    KNN_HIP(hipStreamSynchronize(ix->stream));
+    *fallback_q = acc[0];
+    if (first_fail) *first_fail = acc[2];
+    if (ratio) std::memcpy(ratio, &acc[1], sizeof(float));
+    return KNN_OK;
+}
+
+}  // namespace imgrec

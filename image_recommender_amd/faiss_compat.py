@@ -29,10 +29,16 @@ Exact ties are broken by the smaller label.
 
 All arithmetic runs in the HIP kernels; there is no CPU fallback (``NativeLibraryError`` when the
 library is missing, ``KnnError`` with the C-ABI message on any failure).
+
+Several GPUs from one process: ``devices=[0, 1, ...]`` on any index class (or on ``read_index``), or
+the environment variable ``IMGREC_DEVICES=0,1,...`` for code that cannot pass it — the reference's
+own CLI (main/search_from_image.py:430-441) then searches row shards on every listed GPU
+(include/imgrec_knn.h knn_create_multi); results are the same as on one device.
 """
 from __future__ import annotations
 
 import ctypes as C
+import os
 from types import SimpleNamespace
 
 import numpy as np
@@ -63,17 +69,38 @@ def _ptr(a: np.ndarray) -> C.c_void_p:
     return C.c_void_p(a.ctypes.data)
 
 
-class Index:
-    """Exact flat index on one HIP device (faiss.IndexFlat semantics)."""
+def _device_list(device: int, devices):
+    """The devices an index spans: `devices` if given, else IMGREC_DEVICES when `device` is the
+    default (-1), else None (one device)."""
+    if devices is None and device == -1 and os.environ.get("IMGREC_DEVICES"):
+        devices = [int(v) for v in os.environ["IMGREC_DEVICES"].split(",") if v.strip()]
+    if devices is None:
+        return None
+    devices = [int(v) for v in devices]
+    if not devices:
+        raise ValueError("devices must list at least one device")
+    return devices
 
-    def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1):
+
+class Index:
+    """Exact flat index on one HIP device, or row-sharded over several (faiss.IndexFlat
+    semantics either way)."""
+
+    def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1, devices=None):
         if metric not in _METRIC_TO_KNN:
             raise ValueError(f"unsupported metric {metric}")
         self._h = None
         lib = _lib.load()
         h = C.c_void_p()
-        _lib.check(lib.knn_create(int(d), _METRIC_TO_KNN[metric], int(device), C.byref(h)),
-                   "knn_create")
+        devs = _device_list(device, devices)
+        if devs is not None and len(devs) > 1:
+            arr = (C.c_int * len(devs))(*devs)
+            _lib.check(lib.knn_create_multi(int(d), _METRIC_TO_KNN[metric], arr, len(devs),
+                                            C.byref(h)), "knn_create_multi")
+        else:
+            dev = devs[0] if devs else device
+            _lib.check(lib.knn_create(int(d), _METRIC_TO_KNN[metric], int(dev), C.byref(h)),
+                       "knn_create")
         self._h = h
         self.d = int(d)
         self.metric_type = metric
@@ -108,6 +135,11 @@ class Index:
     @property
     def handle(self) -> C.c_void_p:
         return self._h
+
+    @property
+    def num_shards(self) -> int:
+        """Row shards (devices) the index spans: 1 unless created with several devices."""
+        return int(_lib.load().knn_num_shards(self._h))
 
     # ---- faiss methods ----------------------------------------------------------------------
     def train(self, x) -> None:
@@ -185,28 +217,37 @@ class Index:
         self._mode = mode
 
     def search_stats(self, with_error: bool = False):
-        """(queries of the last search on a candidate path (split / bf16), of which re-run on a
-        more precise path because their certificate failed)
+        """(queries of the last search on a candidate path (split / bf16), of which re-run on the
+        exact kernel because no certificate held)
         [+ largest observed approximation error / certificate bound, with_error=True]."""
-        a, b, r = C.c_int64(), C.c_int64(), C.c_float()
-        _lib.check(_lib.load().knn_search_stats(self._h, C.byref(a), C.byref(b), C.byref(r)),
-                   "knn_search_stats")
-        return (a.value, b.value, r.value) if with_error else (a.value, b.value)
+        st = self.certificate_stats()
+        return ((st["candidate_queries"], st["exact_reruns"], st["max_err_over_bound"])
+                if with_error else (st["candidate_queries"], st["exact_reruns"]))
+
+    def certificate_stats(self) -> dict:
+        """The last search's certificate counts: queries on a candidate path, queries the second
+        chance (all per-split list entries reranked) certified, queries re-run exactly, and the
+        largest observed error / bound.  Waits for that search to finish."""
+        a, b, c, r = C.c_int64(), C.c_int64(), C.c_int64(), C.c_float()
+        _lib.check(_lib.load().knn_search_stats2(self._h, C.byref(a), C.byref(b), C.byref(c),
+                                                 C.byref(r)), "knn_search_stats2")
+        return {"candidate_queries": a.value, "second_chance": c.value, "exact_reruns": b.value,
+                "max_err_over_bound": r.value}
 
 
 class IndexFlat(Index):
-    def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1):
-        super().__init__(d, metric, device)
+    def __init__(self, d: int, metric: int = METRIC_L2, device: int = -1, devices=None):
+        super().__init__(d, metric, device, devices)
 
 
 class IndexFlatL2(Index):
-    def __init__(self, d: int, device: int = -1):
-        super().__init__(d, METRIC_L2, device)
+    def __init__(self, d: int, device: int = -1, devices=None):
+        super().__init__(d, METRIC_L2, device, devices)
 
 
 class IndexFlatIP(Index):
-    def __init__(self, d: int, device: int = -1):
-        super().__init__(d, METRIC_INNER_PRODUCT, device)
+    def __init__(self, d: int, device: int = -1, devices=None):
+        super().__init__(d, METRIC_INNER_PRODUCT, device, devices)
 
 
 class IndexHNSWFlat(IndexFlatL2):
@@ -216,8 +257,9 @@ class IndexHNSWFlat(IndexFlatL2):
     (main/create_index.py:220-221, 231-232) but have no effect on an exact search.
     """
 
-    def __init__(self, d: int, M: int = 32, metric: int = METRIC_L2, device: int = -1):
-        Index.__init__(self, d, metric, device)
+    def __init__(self, d: int, M: int = 32, metric: int = METRIC_L2, device: int = -1,
+                 devices=None):
+        Index.__init__(self, d, metric, device, devices)
         self.hnsw = SimpleNamespace(efConstruction=40, efSearch=16, max_level=0, M=int(M))
 
 
@@ -229,10 +271,10 @@ class IndexIVFPQ(Index):
     """
 
     def __init__(self, quantizer, d: int, nlist: int, m: int, nbits: int = 8,
-                 metric: int = METRIC_L2, device: int = -1):
+                 metric: int = METRIC_L2, device: int = -1, devices=None):
         if d % m != 0:
             raise ValueError(f"IndexIVFPQ: d={d} is not a multiple of m={m}")
-        Index.__init__(self, d, metric, device)
+        Index.__init__(self, d, metric, device, devices)
         self.quantizer = quantizer
         self.nlist, self.pq_m, self.pq_nbits = int(nlist), int(m), int(nbits)
         self.nprobe = 1
@@ -266,9 +308,14 @@ def write_index(index: Index, fname) -> None:
     _lib.check(_lib.load().knn_write(index.handle, str(fname).encode()), "knn_write")
 
 
-def read_index(fname, device: int = -1) -> Index:
+def read_index(fname, device: int = -1, devices=None) -> Index:
     h = C.c_void_p()
-    rc = _lib.load().knn_read(str(fname).encode(), int(device), C.byref(h))
+    devs = _device_list(device, devices)
+    if devs is not None and len(devs) > 1:
+        arr = (C.c_int * len(devs))(*devs)
+        rc = _lib.load().knn_read_multi(str(fname).encode(), arr, len(devs), C.byref(h))
+    else:
+        rc = _lib.load().knn_read(str(fname).encode(), int(devs[0] if devs else device), C.byref(h))
     if rc < 0:
         # faiss raises RuntimeError from read_index; the recommender logs and returns None
         raise KnnError(f"read_index({fname}) failed (code {rc}): {_lib.last_error()}")

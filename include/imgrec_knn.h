@@ -19,17 +19,24 @@
  *   knn_merge_device                     (new) per-shard top-k merge after the RCCL all-gather (§8e)
  *   knn_packed_bytes / knn_merge_packed_device  (new) the same over one packed key|label buffer,
  *                                        so the all-gather is a single collective
+ *   knn_create_multi / knn_read_multi    (new) one index over several devices of one process, so
+ *                                        the reference's single-process CLI
+ *                                        (main/search_from_image.py:430-441) can use every GPU
  *
  * Conventions
  *   - All functions return 0 on success and a negative KNN_E* code on failure; the message of the
  *     last failure on the calling thread is returned by knn_last_error().
  *   - Host-pointer functions (knn_add, knn_search, knn_write, ...) synchronise before returning.
  *     *_device functions take device pointers and a hipStream_t (passed as void*; NULL = the
- *     HIP null stream, like any HIP API) and enqueue asynchronously; they allocate only when the
- *     workspace must grow.  knn_search_device waits once per call on the candidate paths
- *     (bf16 / split) for the uncertified-query count, which a one-lane kernel after the rerank
- *     writes into a pinned host mailbox (the host polls it; no copy, no stream synchronisation),
- *     to decide the re-run; the exact path never waits.
+ *     HIP null stream, like any HIP API), enqueue asynchronously and never wait for the GPU: the
+ *     candidate paths' certificate, its second chance and the exact re-run of the queries it
+ *     cannot settle are all decided on the device.  They allocate only when the workspace must
+ *     grow.
+ *   - Operations on one index may come from different streams and threads: each records an
+ *     event on its stream and an operation on another stream waits for the previous one's first
+ *     (an add on stream A is complete before a search on stream B reads the rows; two searches
+ *     never share the workspace concurrently).  A call on the index's host entry points is
+ *     ordered after earlier device-stream calls the same way.
  *   - Vectors are row-major float32, n rows × d.  Labels are int64.  Result rows are sorted by
  *     ascending distance (L2) or descending inner product (IP/COSINE); exact ties are broken by the
  *     smaller label.  When fewer than k vectors exist, the tail of a result row holds label -1 and
@@ -63,18 +70,22 @@ enum knn_error {
     KNN_ENOSYS = -5    /* not supported (e.g. no GPU visible) */
 };
 
-/* Search arithmetic.  Every mode returns the exact search's results (same labels; distances are
- * fp32 values of the same key): a candidate pass proposes K' rows per query, an fp32 rerank
- * computes their exact keys and a per-query error-bound certificate proves that no row outside
- * the candidates can rank before a returned one; uncertified queries re-run on a more precise
- * path (bf16 -> split when more than 128 fail, else -> exact fp32 kernel).
+/* Search arithmetic.  Every mode returns the exact search's result up to the fp32 tie window:
+ * a candidate pass proposes K' rows per query, an fp32 rerank computes their exact keys and a
+ * per-query error-bound certificate proves that no row outside the candidates can rank before a
+ * returned one.  The returned labels are those of the fp32 keys of the rerank, so they equal the
+ * EXACT mode's labels wherever consecutive keys differ by more than the fp32 evaluation error of
+ * the two summation orders (the rerank's FMA chain vs the MFMA chain: ~1e-6 relative); inside such
+ * a tie window two modes may order near-equal rows differently, never return a row whose exact
+ * distance is farther than the bound.  A query whose certificate fails gets a second chance (every
+ * per-split list entry reranked, certified against the list floor); if that fails too it is
+ * re-run on the exact fp32 kernel, planned on the device.
  * AUTO: the bf16 path (d >= 64; one bf16 MFMA per product, K' = 64) for batches of > 128
  *       queries on an index of >= 16384 rows and for smaller batches on an index of >= 131072
  *       rows (the bf16 copy streams half the bytes); the split path when bf16 is unavailable and
  *       the batch is large; everything else the exact fp32 kernel.
  * EXACT: always the fp32 kernel.  SPLIT: the split path (bf16 hi/lo, three MFMAs per product,
- *       K' = 16/32) whenever k <= 16 and d >= 256.  BF16: the bf16 path for every batch (tests).
- * A candidate-path search waits once per 8192-query chunk for its certificate count. */
+ *       K' = 16/32) whenever k <= 16 and d >= 256.  BF16: the bf16 path for every batch (tests). */
 enum knn_search_mode {
     KNN_SEARCH_AUTO = 0,
     KNN_SEARCH_EXACT = 1,
@@ -87,6 +98,14 @@ enum knn_search_mode {
 
 /* Create an empty index of dimension d on HIP device `device` (-1 = current device). */
 int knn_create(int d, int metric, int device, knn_index_t** out);
+/* Create an empty index whose rows are split over ndev devices (entries may repeat: several
+ * shards on one device).  Every add is cut into ndev contiguous pieces, one per shard; labels are
+ * the dense row offsets as for one device.  A search runs all shards concurrently (each on its own
+ * device and stream) and merges their top-k on devices[0]; *_device pointers live on devices[0].
+ * Every other entry point works unchanged on the returned handle. */
+int knn_create_multi(int d, int metric, const int* devices, int ndev, knn_index_t** out);
+/* Row shards of an index (1 for knn_create). */
+int knn_num_shards(const knn_index_t* index);
 int knn_free(knn_index_t* index);
 
 int knn_dim(const knn_index_t* index);
@@ -133,6 +152,7 @@ int knn_merge_packed_device(const void* packed, int nlists, int64_t nq, int kin,
 /* faiss IndexFlat on-disk layout ("IxF2" for L2, "IxFI" for IP/COSINE). */
 int knn_write(const knn_index_t* index, const char* path);
 int knn_read(const char* path, int device, knn_index_t** out);
+int knn_read_multi(const char* path, const int* devices, int ndev, knn_index_t** out);
 
 /* In-place row normalisation of a host array (faiss.normalize_L2: rows with norm 0 unchanged). */
 int knn_normalize_L2(float* x_host, int64_t n, int d);
@@ -145,12 +165,16 @@ int knn_set_timing(knn_index_t* index, int enable);
 int knn_kernel_time(knn_index_t* index, double* total_ms, int* launches);
 
 int knn_set_search_mode(knn_index_t* index, int mode);
-/* Queries of the last search that took a candidate path (split or bf16), how many of them failed
- * the certificate and were re-run on a more precise path, and (may be NULL) the largest observed
- * |approximate key - fp32 key| / (error bound of both) over all candidates: <= 1 whenever the
- * certificate's bounds hold, in practice far below. */
+/* Queries of the last search that took a candidate path (split or bf16), how many of them were
+ * re-run on the exact kernel because neither certificate held, and (may be NULL) the largest
+ * observed |approximate key - fp32 key| / (error bound of both) over all reranked candidates:
+ * <= 1 whenever the certificate's bounds hold, in practice far below.  Waits for that search.
+ * knn_search_stats2 also returns the queries whose first certificate failed and whose second
+ * chance certified them (may be NULL).  A multi-device index sums re-runs over its shards. */
 int knn_search_stats(knn_index_t* index, int64_t* split_queries, int64_t* fallback_queries,
                      float* max_err_ratio);
+int knn_search_stats2(knn_index_t* index, int64_t* split_queries, int64_t* fallback_queries,
+                      int64_t* second_chance_queries, float* max_err_ratio);
 
 /* Arithmetic the last search's first query chunk ran: 0 = exact fp32 kernel, 1 = split path,
  * 2 = bf16 path (the candidate paths' fallbacks are counted by knn_search_stats). */

@@ -96,8 +96,8 @@ def test_bf16_concat_layout_self_query(faiss):
 
 
 def test_bf16_cascade_through_split_on_ties(faiss):
-    """Every row duplicated 80 times (more than K' = 64): no certificate can hold; 150 > 128
-    failures cascade to the split path, which fails too and re-runs exactly; ties still break by
+    """Every row duplicated 80 times (more than K' = 64): the first certificate cannot hold for any
+    query; the second chance or the device-planned exact re-run settles each; ties still break by
     the smaller label."""
     base = mixture(200, 256, centres=20, seed=9)
     xb = np.repeat(base, 80, axis=0)
@@ -106,8 +106,8 @@ def test_bf16_cascade_through_split_on_ties(faiss):
     idx.add(xb)
     idx.search_mode = "bf16"
     D, I = idx.search(xq, 10)
-    ncand, nfb = idx.search_stats()
-    assert ncand == 150 and nfb == 150
+    st = idx.certificate_stats()
+    assert st["candidate_queries"] == 150 and st["second_chance"] + st["exact_reruns"] == 150
     check_knn(D, I, xb, xq, 10, "l2")
     assert (I == np.arange(150)[:, None] * 80 + np.arange(10)[None, :]).all()
 
@@ -123,8 +123,8 @@ def test_bf16_partial_fallback_matches_exact(faiss):
     idx.add(xb)
     idx.search_mode = "bf16"
     D, I = idx.search(xq, 10)
-    ncand, nfb = idx.search_stats()
-    assert ncand == 290 and 40 <= nfb < 290
+    st = idx.certificate_stats()
+    assert st["candidate_queries"] == 290 and 40 <= st["second_chance"] + st["exact_reruns"] < 290
     check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
     idx.search_mode = "exact"
     De, Ie = idx.search(xq, 10)
@@ -285,11 +285,11 @@ def test_bf16_cluster_sorted_storage(faiss, nq):
     assert nfb <= nq // 20
 
 
-def test_bf16_stats_mailbox_per_search(faiss):
-    """The certificate stats reach the host through a pinned mailbox and the device counters are
-    zeroed after every rerank: an all-failing search followed by a clean one reports 0 fallbacks,
-    and two indexes searched in turn keep their own counts (csrc/knn_refine.hip
-    publish_stats_kernel, csrc/knn_capi.cpp read_stats)."""
+def test_bf16_stats_per_search(faiss):
+    """The certificate counters are per search and per index: the device-side fold (two chunk
+    parities + per-search totals, csrc/knn_refine.hip fallback_prep_kernel) resets them, so an
+    all-failing search followed by a clean one reports 0, and two indexes searched in turn keep
+    their own counts (knn_search_stats2 waits for the search it reports)."""
     base = mixture(200, 256, centres=20, seed=19)
     dup = faiss.IndexFlatL2(256)
     dup.add(np.repeat(base, 80, axis=0))                 # 80 copies of each row: no certificate
@@ -302,7 +302,8 @@ def test_bf16_stats_mailbox_per_search(faiss):
     qc = mixture(200, 256, centres=60, seed=21)
     for _ in range(3):
         dup.search(qd, 10)
-        assert tuple(dup.search_stats()) == (40, 40)
+        st = dup.certificate_stats()
+        assert st["candidate_queries"] == 40 and st["second_chance"] + st["exact_reruns"] == 40
         D, I = clean.search(qc, 10)
         ncand, nfb = clean.search_stats()
         assert ncand == 200 and nfb <= 4
@@ -311,7 +312,8 @@ def test_bf16_stats_mailbox_per_search(faiss):
     D, I = dup.search(qd, 10)
     assert (I == np.arange(40)[:, None] * 80 + np.arange(10)[None, :]).all()
     dup.search(qd[:1], 10)
-    assert tuple(dup.search_stats()) == (1, 1)
+    st = dup.certificate_stats()
+    assert st["candidate_queries"] == 1 and st["second_chance"] + st["exact_reruns"] == 1
 
 
 def test_bf16_two_query_chunks(faiss):

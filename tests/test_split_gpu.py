@@ -110,8 +110,8 @@ def test_split_certificate_fallback_on_ties(faiss):
     idx.add(xb)
     idx.search_mode = "split"
     D, I = idx.search(xq, 10)
-    nsplit, nfb = idx.search_stats()
-    assert nsplit == 150 and nfb == 150
+    st = idx.certificate_stats()      # first certificate failed for all; second chance or re-run
+    assert st["candidate_queries"] == 150 and st["second_chance"] + st["exact_reruns"] == 150
     check_knn(D, I, xb, xq, 10, "l2")
     assert (I == np.arange(150)[:, None] * 40 + np.arange(10)[None, :]).all()
 
@@ -127,8 +127,8 @@ def test_split_partial_fallback_matches_exact(faiss):
     idx.add(xb)
     idx.search_mode = "split"
     D, I = idx.search(xq, 10)
-    nsplit, nfb = idx.search_stats()
-    assert nsplit == 300 and 100 <= nfb < 300
+    st = idx.certificate_stats()
+    assert st["candidate_queries"] == 300 and 100 <= st["second_chance"] + st["exact_reruns"] < 300
     check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
     idx.search_mode = "exact"
     De, Ie = idx.search(xq, 10)
