@@ -119,6 +119,7 @@ struct knn_index {
     float* cand2_d = nullptr; size_t cand2_d_cap = 0;
     int64_t* cand2_i = nullptr; size_t cand2_i_cap = 0;
     int* fail = nullptr; size_t fail_cap = 0;          // the uncertified queries of a chunk
+    int* chance = nullptr; size_t chance_cap = 0;      // the second-chance queue of a chunk
     int* stat = nullptr;                               // 12 ints: two chunk parities + totals
     int stat_seq = 0;                                  // chunks run (parity = seq & 1)
     bool stat_valid = false;                           // the last search ran a candidate path

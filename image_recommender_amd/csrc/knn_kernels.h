@@ -62,8 +62,10 @@ struct RerankArgs {
     int64_t* I;
     int* stats;                 // this chunk's device counters (zero on entry): [0] queries left
                                 // for the exact re-run, [1] max observed error / bound (float
-                                // bits, atomicMax), [2] queries whose first certificate failed
+                                // bits, atomicMax), [2] queries whose first certificate failed,
+                                // [3] of those, queued for the second chance
     int* fail_list;             // nq entries: the queries left for the exact re-run
+    int* chance_list = nullptr; // nq entries: the second-chance queue (raw_d set)
     // the candidate pass's raw per-split lists (second chance; NULL = none): raw_lists sorted
     // lists of raw_km entries per query, query q's at q * raw_stride_q (global labels, -1 empty)
     const float* raw_d = nullptr;

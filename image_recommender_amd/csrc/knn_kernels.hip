@@ -23,6 +23,7 @@
 // operands, so the contraction is unchanged).
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <type_traits>
 #include <stdint.h>
 #include <float.h>
@@ -587,24 +588,20 @@ __device__ __forceinline__ void wave_select(float (&kd)[KM], int64_t (&ki)[KM], 
     }
 }
 
+// One query (WPQ = 4) or four (WPQ = 1) of knn_merge_kernel; block-uniform control flow (no
+// wave leaves before the block's __syncthreads).
 template <int KM, int WPQ>
-__global__ void __launch_bounds__(256)
-knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
-                 int nlists, int kin, int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
-                 int metric, int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
-                 float* __restrict__ floor_out, const int* __restrict__ dyn, int dyn_lists,
-                 const int* __restrict__ out_rows) {
+__device__ __forceinline__ void merge_block(const float* __restrict__ cd, const int64_t* __restrict__ ci,
+                                            int64_t blk, int64_t nq, int nlists, int kin,
+                                            int64_t stride_q, int64_t stride_l, int64_t stride_li,
+                                            int k, int metric, int negate_in, float* __restrict__ D,
+                                            int64_t* __restrict__ I, float* __restrict__ floor_out,
+                                            const int* __restrict__ out_rows,
+                                            float (&sd)[4][KM], int64_t (&si)[4][KM]) {
     constexpr int QPB = 4 / WPQ;                     // queries per 256-thread block
-    if (dyn) {                                       // device-planned lists (exact re-run)
-        nq = dyn[0];
-        nlists = dyn[2] * dyn_lists;
-        stride_q = dyn[3];
-    }
-    __shared__ float sd[4][KM];
-    __shared__ int64_t si[4][KM];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int64_t q = (int64_t)blockIdx.x * QPB + wave / WPQ;
+    const int64_t q = blk * QPB + wave / WPQ;
     const int sub = wave % WPQ;
     const bool active = q < nq;
 
@@ -662,19 +659,47 @@ knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, i
     // WPQ == 4: one query per block; every wave's top-k to LDS, wave 0 merges the 4k.
     wave_select<KM>(kd, ki, k, lane, sd[wave], si[wave], 0, metric);
     __syncthreads();
-    if (wave != 0 || !active) return;
+    if (wave == 0 && active) {
 #pragma unroll
-    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
-    if (lane < 4) {
-        for (int r = 0; r < k; ++r) {
-            const float d = sd[lane][r];
-            const int64_t id = si[lane][r];
-            if (id < 0) break;
-            list_insert<KM, int64_t>(kd, ki, d, id);
+        for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+        if (lane < 4) {
+            for (int r = 0; r < k; ++r) {
+                const float d = sd[lane][r];
+                const int64_t id = si[lane][r];
+                if (id < 0) break;
+                list_insert<KM, int64_t>(kd, ki, d, id);
+            }
         }
+        const int64_t orow = out_rows ? (int64_t)out_rows[q] : q;
+        wave_select<KM>(kd, ki, k, lane, D + orow * k, I + orow * k, 1, metric);
     }
-    const int64_t orow = out_rows ? (int64_t)out_rows[q] : q;
-    wave_select<KM>(kd, ki, k, lane, D + orow * k, I + orow * k, 1, metric);
+}
+
+// dyn (device-planned lists of the exact re-run): nq, lists and stride come from dyn, and the
+// grid (fixed, small: a near-empty launch when nothing is re-run) loops over the queries.
+template <int KM, int WPQ>
+__global__ void __launch_bounds__(256)
+knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
+                 int nlists, int kin, int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
+                 int metric, int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
+                 float* __restrict__ floor_out, const int* __restrict__ dyn, int dyn_lists,
+                 const int* __restrict__ out_rows) {
+    __shared__ float sd[4][KM];
+    __shared__ int64_t si[4][KM];
+    if (!dyn) {
+        merge_block<KM, WPQ>(cd, ci, blockIdx.x, nq, nlists, kin, stride_q, stride_l, stride_li, k,
+                             metric, negate_in, D, I, floor_out, out_rows, sd, si);
+        return;
+    }
+    nq = dyn[0];
+    nlists = dyn[2] * dyn_lists;
+    stride_q = dyn[3];
+    constexpr int QPB = 4 / WPQ;
+    for (int64_t blk = blockIdx.x; blk * QPB < nq; blk += gridDim.x) {
+        merge_block<KM, WPQ>(cd, ci, blk, nq, nlists, kin, stride_q, stride_l, stride_li, k, metric,
+                             negate_in, D, I, floor_out, out_rows, sd, si);
+        __syncthreads();                          // sd / si reused by the next query
+    }
 }
 
 __global__ void fill_empty_kernel(float* __restrict__ D, int64_t* __restrict__ I, int64_t n,
@@ -990,8 +1015,8 @@ hipError_t launch_merge_dyn(const float* cd, const int64_t* ci, const int* dyn, 
                             int kin, int64_t cap_q, int k, int metric, const int* out_rows,
                             float* D, int64_t* I, hipStream_t st) {
     if (cap_q <= 0) return hipSuccess;
-    // four waves per query: the plan can give one query block all the row splits
-    const dim3 grid((unsigned)cap_q), block(256);
+    // four waves per query (the plan can give one query block all the row splits); the grid loops
+    const dim3 grid((unsigned)std::min<int64_t>(cap_q, 256)), block(256);
 #define IMGREC_MERGE_DYN(KMV)                                                                      \
     hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, cap_q, 0, kin,      \
                        (int64_t)0, (int64_t)kin, (int64_t)kin, k, metric, 0, D, I, nullptr, dyn,   \

@@ -25,6 +25,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "knn_kernels.h"
 #include "wave_ops.h"
@@ -191,24 +192,113 @@ __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
     return d1 < d2 || (d1 == d2 && i1 < i2);
 }
 
+constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
+
+// Error bounds of one query's certificate (DESIGN.md "bf16 path" / "Split path").
+struct QueryBounds {
+    float qn, xm, nn, e_ip, c_fp;
+    int metric;
+    static constexpr float u = 1.0f / 8388608.f;   // 2^-23
+    __device__ __forceinline__ QueryBounds(const RerankArgs& a, int64_t q) {
+        metric = a.metric;
+        qn = a.qnorm[q];
+        xm = *a.xn_max;
+        c_fp = a.c_fp;
+        nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
+        // |approximate q.x - q.x| for every row:
+        //   split: c_split |q| max|x|
+        //   bf16:  |q.(x - xh) + (q - qh).xh| + accumulation <= |q| R + dq (X + R) + c_acc |qh| |xh|
+        //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max
+        //          |x|, |qh| <= |q| + dq, |xh| <= X + R), inflated for the bound's fp32 evaluation
+        if (a.mode == kModeBF16) {
+            const float sq = sqrtf(qn), X = sqrtf(xm), R = *a.xr_max, dq = a.q_resid[q];
+            e_ip = (sq * R + dq * (X + R) + a.c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
+        } else {
+            e_ip = a.c_split * nn;
+        }
+    }
+    // |approx key - exact key| bound at key v
+    __device__ __forceinline__ float bound_a(float v) const {
+        return metric == 1 ? 2.f * e_ip + 2.f * u * (qn + xm + fabsf(v)) : e_ip;
+    }
+    // |fp32 rerank key - exact key| bound
+    __device__ __forceinline__ float bound_f(float v) const {
+        return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
+    }
+    // candidates with approximate key above this cannot reach the top k (the k best by
+    // approximate key have exact keys <= a_k + E_a)
+    __device__ __forceinline__ float prefix_limit(float a_k) const {
+        return a_k + 2.02f * (bound_a(a_k) + bound_f(a_k));
+    }
+};
+
+// Exact fp32 dot products of one query with kRerankRows rows, one wave, lane-strided float4
+// chunks (x y z w FMAs) then a butterfly: a row's key has the same bits in every pass.
+// IT > 0: the query's chunks are in registers (qr); IT = 0: streamed with the rows.
+template <int IT>
+__device__ __forceinline__ void rerank_dots(const float4* __restrict__ q4, const float4 (&qr)[IT > 0 ? IT : 1],
+                                            int n4, int lane, const float4* const (&r4)[kRerankRows],
+                                            float (&acc)[kRerankRows]) {
+#pragma unroll
+    for (int v = 0; v < kRerankRows; ++v) acc[v] = 0.f;
+    if constexpr (IT > 0) {
+        float4 b[kRerankRows][IT];
+#pragma unroll
+        for (int v = 0; v < kRerankRows; ++v)
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int i = lane + 64 * it;
+                b[v][it] = i < n4 ? r4[v][i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                acc[v] = fmaf(qr[it].x, b[v][it].x, acc[v]);
+                acc[v] = fmaf(qr[it].y, b[v][it].y, acc[v]);
+                acc[v] = fmaf(qr[it].z, b[v][it].z, acc[v]);
+                acc[v] = fmaf(qr[it].w, b[v][it].w, acc[v]);
+            }
+    } else {
+#pragma unroll 4
+        for (int i = lane; i < n4; i += 64) {
+            const float4 qa = q4[i];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                const float4 bb = r4[v][i];
+                acc[v] = fmaf(qa.x, bb.x, acc[v]);
+                acc[v] = fmaf(qa.y, bb.y, acc[v]);
+                acc[v] = fmaf(qa.z, bb.z, acc[v]);
+                acc[v] = fmaf(qa.w, bb.w, acc[v]);
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < kRerankRows; ++v)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
+}
+
+__device__ __forceinline__ float rerank_key(float ip, float qn, float xnr, int metric) {
+    if (metric == 1) {
+        const float kv = fmaf(-2.f, ip, qn + xnr);
+        return kv < 0.f ? 0.f : kv;
+    }
+    return -ip;
+}
+
 // One workgroup of kRerankWaves waves per query.  a.cd/a.ci: the merged approximate candidates,
 // nq x kc, ascending raw keys (L2 distance or -ip), empty = label -1.
 // IT > 0: the query row sits in registers (IT float4 per lane, dp <= 256 IT) and every wave loads
 // its candidates' rows kRerankRows at a time, all loads in flight at once; IT = 0 streams the
 // query with the rows (any dp).
-//
-// A query whose certificate fails gets a second chance in the same workgroup (a.raw_d != NULL):
-// every entry of the candidate pass's per-split lists (not only the merged K' = 64) that can
-// still rank in the top k is reranked, and the certificate is re-run with the list floor alone
-// (the smallest last key of a full list: every row outside all lists is at least that).  Only if
-// that fails too is the query listed for the exact fp32 re-run (run_fallback, on device).
-constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
+// A query whose certificate fails goes to the second-chance queue (a.raw_d set: stats[3] counts
+// it) or straight to the exact re-run list (stats[0]).
 template <int IT>
 __global__ void __launch_bounds__(kRerankWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
 rerank_certify_kernel(const RerankArgs a) {
     __shared__ float skey[64];
     __shared__ int64_t slab[64];
-    __shared__ int s_fail;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int64_t q = blockIdx.x;
@@ -216,54 +306,24 @@ rerank_certify_kernel(const RerankArgs a) {
     const int64_t id_offset = a.id_offset;
     const float* __restrict__ cd = a.cd;
     const int64_t* __restrict__ ci = a.ci;
-    const float* __restrict__ xb = a.xb;
-    const float* __restrict__ xn = a.xn;
-    const float* qv = a.qp + q * dp;
-    const float qn = a.qnorm[q];
     const int64_t lab = lane < kc ? ci[q * kc + lane] : (int64_t)-1;
     const float ak = lane < kc ? cd[q * kc + lane] : INFINITY;   // approximate key, ascending
     const bool valid = lab >= 0;
     const int nvalid = __popcll(__ballot(valid));               // valid candidates come first
+    const QueryBounds B(a, q);
 
-    const float xm = *a.xn_max;
-    const float nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
-    const float u = 1.0f / 8388608.f;               // 2^-23
-    // |approximate q.x - q.x| for every row:
-    //   split: c_split |q| max|x|
-    //   bf16:  |q.(x - xh) + (q - qh).xh| + accumulation <= |q| R + dq (X + R) + c_acc |qh| |xh|
-    //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max |x|,
-    //          |qh| <= |q| + dq, |xh| <= X + R), inflated for the fp32 evaluation of the bound
-    float e_ip;
-    if (a.mode == kModeBF16) {
-        const float sq = sqrtf(qn), X = sqrtf(xm), R = *a.xr_max, dq = a.q_resid[q];
-        e_ip = (sq * R + dq * (X + R) + a.c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
-    } else {
-        e_ip = a.c_split * nn;
-    }
-    const float c_fp = a.c_fp;
-    auto bound_a = [&](float v) {                   // |approx key - exact key| bound at key v
-        return metric == 1 ? 2.f * e_ip + 2.f * u * (qn + xm + fabsf(v)) : e_ip;
-    };
-    auto bound_f = [&](float v) {                   // |fp32 rerank key - exact key| bound
-        return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
-    };
-
-    // Only a prefix of the (ascending) candidates can hold the answer: the k best by approximate
-    // key have exact keys <= a_k + E_a, so a candidate whose approximate key exceeds
-    // a_k + 2 (E_a + E_f) cannot rank before them.  The prefix P = {approx <= that} is reranked;
-    // the first candidate left out bounds every excluded candidate's approximate key from below.
+    // Only a prefix of the (ascending) candidates can hold the answer; the prefix P = {approx <=
+    // prefix_limit(a_k)} is reranked and the first candidate left out bounds every excluded
+    // candidate's approximate key from below.
     int m = nvalid;
-    float thr = INFINITY;
     if (nvalid >= k) {
-        const float a_k = __shfl(ak, k - 1, 64);
-        thr = a_k + 2.02f * (bound_a(a_k) + bound_f(a_k));
+        const float thr = B.prefix_limit(__shfl(ak, k - 1, 64));
         m = __popcll(__ballot(valid && ak <= thr));
     }
 
-    // exact fp32 dot products, kRerankRows rows per wave at a time; a row's sum has the same
-    // order wherever and in whichever pass it runs, so its key is the same bits
+    // exact fp32 keys of the prefix: candidate c goes to wave c % kRerankWaves
     const int n4 = dp / 4;
-    const float4* q4 = reinterpret_cast<const float4*>(qv);
+    const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
     float4 qr[IT > 0 ? IT : 1];
     if constexpr (IT > 0) {
 #pragma unroll
@@ -272,130 +332,83 @@ rerank_certify_kernel(const RerankArgs a) {
             qr[it] = i < n4 ? q4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    auto dots = [&](const float4* const (&r4)[kRerankRows], float (&acc)[kRerankRows])
-        __attribute__((always_inline)) {
-#pragma unroll
-        for (int v = 0; v < kRerankRows; ++v) acc[v] = 0.f;
-        if constexpr (IT > 0) {
-            float4 b[kRerankRows][IT];
-#pragma unroll
-            for (int v = 0; v < kRerankRows; ++v)
-#pragma unroll
-                for (int it = 0; it < IT; ++it) {
-                    const int i = lane + 64 * it;
-                    b[v][it] = i < n4 ? r4[v][i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-#pragma unroll
-            for (int it = 0; it < IT; ++it)
-#pragma unroll
-                for (int v = 0; v < kRerankRows; ++v) {
-                    acc[v] = fmaf(qr[it].x, b[v][it].x, acc[v]);
-                    acc[v] = fmaf(qr[it].y, b[v][it].y, acc[v]);
-                    acc[v] = fmaf(qr[it].z, b[v][it].z, acc[v]);
-                    acc[v] = fmaf(qr[it].w, b[v][it].w, acc[v]);
-                }
-        } else {
-#pragma unroll 4
-            for (int i = lane; i < n4; i += 64) {
-                const float4 qa = q4[i];
-#pragma unroll
-                for (int v = 0; v < kRerankRows; ++v) {
-                    const float4 bb = r4[v][i];
-                    acc[v] = fmaf(qa.x, bb.x, acc[v]);
-                    acc[v] = fmaf(qa.y, bb.y, acc[v]);
-                    acc[v] = fmaf(qa.z, bb.z, acc[v]);
-                    acc[v] = fmaf(qa.w, bb.w, acc[v]);
-                }
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < kRerankRows; ++v)
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
-    };
-    auto key_of = [&](float ip, int64_t l) __attribute__((always_inline)) {
-        if (metric == 1) {
-            const float kv = fmaf(-2.f, ip, qn + xn[l - id_offset]);
-            return kv < 0.f ? 0.f : kv;
-        }
-        return -ip;
-    };
-    auto row_ptr = [&](int64_t l) __attribute__((always_inline)) {
-        return reinterpret_cast<const float4*>(xb + (l - id_offset) * dp);
-    };
-    auto lane_label = [&](int c) __attribute__((always_inline)) {
+    auto row_of = [&](int c) {
         const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
         const int hi32 = __shfl((int)(lab >> 32), c, 64);
-        return ((int64_t)hi32 << 32) | (uint32_t)lo32;
+        const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
+        return reinterpret_cast<const float4*>(a.xb + (l - id_offset) * dp);
     };
-    // the prefix: candidate c goes to wave c % kRerankWaves, sits in lane c
     for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
         const float4* r4[kRerankRows];
         float acc[kRerankRows];
 #pragma unroll
-        for (int v = 0; v < kRerankRows; ++v)      // clamped: loads unconditional
-            r4[v] = row_ptr(lane_label(min(c0 + kRerankWaves * v, m - 1)));
-        dots(r4, acc);
+        for (int v = 0; v < kRerankRows; ++v)
+            r4[v] = row_of(min(c0 + kRerankWaves * v, m - 1));   // clamped: loads unconditional
+        rerank_dots<IT>(q4, qr, n4, lane, r4, acc);
 #pragma unroll
         for (int v = 0; v < kRerankRows; ++v) {
             const int c = c0 + kRerankWaves * v;
-            if (lane == c && c < m) skey[c] = key_of(acc[v], lab);
+            if (lane == c && c < m) skey[c] = rerank_key(acc[v], B.qn, a.xn[lab - id_offset], metric);
         }
     }
     if (wave == 0) slab[lane] = lab;
     __syncthreads();
+    if (wave != 0) return;
+    const float key = lane < m ? skey[lane] : INFINITY;
 
-    if (wave == 0) {
-        const float key = lane < m ? skey[lane] : INFINITY;
-        // rank of this lane's candidate inside the prefix by (key, label)
-        const bool inP = lane < m;
-        int rank = 0;
-        for (int i = 0; i < m; ++i)
-            if (inP && ranks_before_r(skey[i], slab[i], key, lab)) ++rank;
-        if (inP && rank < k) {
-            a.D[q * k + rank] = (metric == 1) ? key : -key;
-            a.I[q * k + rank] = lab;
-        }
-        if (lane >= m && lane < k) {
-            a.D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
-            a.I[q * k + lane] = -1;
-        }
-        // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
-        // whenever the bounds hold; reported by knn_search_stats so tests and the bench watch it)
-        if (inP) {
-            const float r = fabsf(ak - key) / (bound_a(ak) + bound_f(key));
-            atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
-        }
-        // certificate: tau = smallest approximate key a row outside the prefix can have — the
-        // K'-th candidate's (when the set is full), the merge floor (rows dropped by full lists)
-        // and the first candidate left out of the prefix; +inf means every row was reranked
-        const int64_t lab_tau = ci[q * kc + kc - 1];
-        float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
-        if (a.floor) tau = fminf(tau, a.floor[q]);
-        const float a_out = __shfl(ak, min(m, 63), 64);
-        if (m < nvalid) tau = fminf(tau, a_out);
-        bool failed = false;                        // tau = +inf: every row was reranked
-        if (tau != INFINITY) {
-            float sk = (inP && rank == k - 1) ? key : -INFINITY;
+    // rank of this lane's candidate inside the prefix by (key, label)
+    const bool inP = lane < m;
+    int rank = 0;
+    for (int i = 0; i < m; ++i)
+        if (inP && ranks_before_r(skey[i], slab[i], key, lab)) ++rank;
+    if (inP && rank < k) {
+        a.D[q * k + rank] = (metric == 1) ? key : -key;
+        a.I[q * k + rank] = lab;
+    }
+    if (lane >= m && lane < k) {
+        a.D[q * k + lane] = (metric == 1) ? FLT_MAX : -FLT_MAX;
+        a.I[q * k + lane] = -1;
+    }
+
+    // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
+    // whenever the bounds hold; reported by knn_search_stats so tests and the bench watch it)
+    if (inP) {
+        const float r = fabsf(ak - key) / (B.bound_a(ak) + B.bound_f(key));
+        atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+    }
+
+    // certificate: tau = smallest approximate key a row outside the prefix can have — the K'-th
+    // candidate's (when the set is full), the merge floor (rows dropped by full lists) and the
+    // first candidate left out of the prefix; +inf means every row was reranked
+    const int64_t lab_tau = ci[q * kc + kc - 1];
+    float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
+    if (a.floor) tau = fminf(tau, a.floor[q]);
+    const float a_out = __shfl(ak, min(m, 63), 64);
+    if (m < nvalid) tau = fminf(tau, a_out);
+    bool failed = false;                            // tau = +inf: every row was reranked
+    if (tau != INFINITY) {
+        float sk = (inP && rank == k - 1) ? key : -INFINITY;
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
-            // fewer than k reranked rows while rows were left out: nothing to certify with
-            failed = !(m >= k && (tau - bound_a(tau)) > (sk + bound_f(sk)));
-        }
-        if (lane == 0) s_fail = failed ? 1 : 0;
+        for (int off = 32; off > 0; off >>= 1) sk = fmaxf(sk, __shfl_xor(sk, off, 64));
+        // fewer than k reranked rows while rows were left out: nothing to certify with
+        failed = !(m >= k && (tau - B.bound_a(tau)) > (sk + B.bound_f(sk)));
     }
-    __syncthreads();
-    if (!s_fail) return;
-    if (!a.raw_d) {
-        if (threadIdx.x == 0) {
-            atomicAdd(a.stats + 2, 1);
-            a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
-        }
-        return;
+    if (failed && lane == 0) {
+        atomicAdd(a.stats + 2, 1);
+        if (a.raw_d) a.chance_list[atomicAdd(a.stats + 3, 1)] = (int)q;
+        else a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
     }
+}
 
-    // ---- second chance: every per-split list entry with approximate key <= thr (those above it
-    // cannot reach the top k, by the prefix argument), certified against the list floor --------
+// Second chance for the queries the rerank could not certify (stats[3] of them in chance_list):
+// every entry of the candidate pass's per-split lists with approximate key <= the prefix limit
+// (those above it cannot reach the top k) is reranked, and the certificate is re-run against
+// the list floor alone — the smallest last key of a full list, below which no row outside all
+// lists can be.  A workgroup per listed query, the grid looping over the list (a fixed, small
+// grid: with nothing listed the launch is a few microseconds).  Queries it cannot settle go to
+// the exact re-run list (stats[0]).
+__global__ void __launch_bounds__(kRerankWaves * 64)
+second_chance_kernel(const RerankArgs a) {
     __shared__ float w_key[kWideCap], w_apx[kWideCap];
     __shared__ int64_t w_lab[kWideCap];
     __shared__ float o_key[64];
@@ -404,76 +417,92 @@ rerank_certify_kernel(const RerankArgs a) {
     __shared__ unsigned w_tau;
     __shared__ float s_sk;
     constexpr int NT = kRerankWaves * 64;
-    const int t = threadIdx.x;
-    if (t == 0) {
-        w_n = 0;
-        w_tau = key_bits_ordered(INFINITY);
-        s_sk = -INFINITY;
-        atomicAdd(a.stats + 2, 1);
-    }
-    if (t < 64) o_lab[t] = -1;
-    __syncthreads();
-    const float* rd = a.raw_d + q * a.raw_stride_q;
-    const int64_t* ri = a.raw_i + q * a.raw_stride_q;
-    const int km = a.raw_km, ne = a.raw_lists * km;
-    for (int l = t; l < a.raw_lists; l += NT) {
-        const int e = l * km + km - 1;
-        if (ri[e] >= 0) atomicMin(&w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
-    }
-    for (int e = t; e < ne; e += NT) {
-        const int64_t l = ri[e];
-        const float v = rd[e];
-        if (l >= 0 && v <= thr) {
-            const int s = atomicAdd(&w_n, 1);
-            if (s < kWideCap) { w_apx[s] = v; w_lab[s] = l; }
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int count = a.stats[3];
+    const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc;
+    const int n4 = dp / 4;
+    const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
+    for (int item = blockIdx.x; item < count; item += gridDim.x) {
+        const int64_t q = a.chance_list[item];
+        const QueryBounds B(a, q);
+        // the same prefix limit as the first pass, from the merged candidates' k-th key
+        const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
+        const float thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
+        if (t == 0) {
+            w_n = 0;
+            w_tau = key_bits_ordered(INFINITY);
+            s_sk = -INFINITY;
         }
-    }
-    __syncthreads();
-    const int n = w_n;
-    bool ok = n <= kWideCap;
-    if (ok) {
-        for (int c0 = wave; c0 < n; c0 += kRerankWaves * kRerankRows) {
-            const float4* r4[kRerankRows];
-            float acc[kRerankRows];
-#pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) r4[v] = row_ptr(w_lab[min(c0 + kRerankWaves * v, n - 1)]);
-            dots(r4, acc);
-#pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
-                const int c = c0 + kRerankWaves * v;
-                if (lane == 0 && c < n) w_key[c] = key_of(acc[v], w_lab[c]);
+        if (t < 64) o_lab[t] = -1;
+        __syncthreads();
+        const float* rd = a.raw_d + q * a.raw_stride_q;
+        const int64_t* ri = a.raw_i + q * a.raw_stride_q;
+        const int km = a.raw_km, ne = a.raw_lists * km;
+        for (int l = t; l < a.raw_lists; l += NT) {
+            const int e = l * km + km - 1;
+            if (ri[e] >= 0) atomicMin(&w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
+        }
+        for (int e = t; e < ne; e += NT) {
+            const int64_t l = ri[e];
+            const float v = rd[e];
+            if (l >= 0 && v <= thr) {
+                const int s = atomicAdd(&w_n, 1);
+                if (s < kWideCap) { w_apx[s] = v; w_lab[s] = l; }
             }
         }
         __syncthreads();
-        // rank of every reranked entry by (key, label): labels are distinct (a row sits in one list)
-        for (int s = t; s < n; s += NT) {
-            const float kv = w_key[s];
-            const int64_t lb = w_lab[s];
-            int rank = 0;
-            for (int j = 0; j < n && rank < k; ++j) rank += ranks_before_r(w_key[j], w_lab[j], kv, lb) ? 1 : 0;
-            if (rank < k) {
-                o_key[rank] = kv;
-                o_lab[rank] = lb;
-                if (rank == k - 1) s_sk = kv;
+        const int n = w_n;
+        bool ok = n <= kWideCap;
+        if (ok) {
+            const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
+            for (int c0 = wave; c0 < n; c0 += kRerankWaves * kRerankRows) {
+                const float4* r4[kRerankRows];
+                float acc[kRerankRows];
+#pragma unroll
+                for (int v = 0; v < kRerankRows; ++v)
+                    r4[v] = reinterpret_cast<const float4*>(
+                        a.xb + (w_lab[min(c0 + kRerankWaves * v, n - 1)] - a.id_offset) * dp);
+                rerank_dots<0>(q4, none, n4, lane, r4, acc);
+#pragma unroll
+                for (int v = 0; v < kRerankRows; ++v) {
+                    const int c = c0 + kRerankWaves * v;
+                    if (lane == 0 && c < n)
+                        w_key[c] = rerank_key(acc[v], B.qn, a.xn[w_lab[c] - a.id_offset], metric);
+                }
             }
-            const float r = fabsf(w_apx[s] - kv) / (bound_a(w_apx[s]) + bound_f(kv));
-            atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+            __syncthreads();
+            // rank of every reranked entry by (key, label): labels are distinct (a row sits in
+            // one list)
+            for (int s = t; s < n; s += NT) {
+                const float kv = w_key[s];
+                const int64_t lb = w_lab[s];
+                int rank = 0;
+                for (int j = 0; j < n && rank < k; ++j) rank += ranks_before_r(w_key[j], w_lab[j], kv, lb) ? 1 : 0;
+                if (rank < k) {
+                    o_key[rank] = kv;
+                    o_lab[rank] = lb;
+                    if (rank == k - 1) s_sk = kv;
+                }
+                const float r = fabsf(w_apx[s] - kv) / (B.bound_a(w_apx[s]) + B.bound_f(kv));
+                atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+            }
+            __syncthreads();
+            // +inf floor: no list dropped a row, so every row was a candidate and W holds all
+            // that can matter
+            const float tauL = key_from_ordered(w_tau);
+            ok = tauL == INFINITY || (tauL - B.bound_a(tauL)) > (s_sk + B.bound_f(s_sk));
         }
-        __syncthreads();
-        // every row outside the lists has approximate key >= the floor (+inf: no list dropped a
-        // row, so every row of the corpus was a candidate and W holds all that can matter)
-        const float tauL = key_from_ordered(w_tau);
-        ok = tauL == INFINITY || (tauL - bound_a(tauL)) > (s_sk + bound_f(s_sk));
-    }
-    if (ok) {
-        if (t < k) {
-            const int64_t lb = o_lab[t];
-            a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
-                                    : ((metric == 1) ? o_key[t] : -o_key[t]);
-            a.I[q * k + t] = lb;
+        if (ok) {
+            if (t < k) {
+                const int64_t lb = o_lab[t];
+                a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
+                                        : ((metric == 1) ? o_key[t] : -o_key[t]);
+                a.I[q * k + t] = lb;
+            }
+        } else if (t == 0) {
+            a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
         }
-    } else if (t == 0) {
-        a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
+        __syncthreads();                // LDS reused by the next item
     }
 }
 
@@ -502,7 +531,7 @@ fallback_prep_kernel(int* __restrict__ stat, int parity, int first, const int* _
         acc[1] = first ? sp[1] : max(acc[1], sp[1]);        // ratio >= 0: bit order = float order
         acc[2] = first ? sp[2] : acc[2] + sp[2];
         int* other = stat + 4 * (parity ^ 1);
-        other[0] = 0; other[1] = 0; other[2] = 0;
+        other[0] = 0; other[1] = 0; other[2] = 0; other[3] = 0;
     }
     const int lane = threadIdx.x & 63;
     const int64_t rows = (int64_t)nqb * 32;
@@ -577,7 +606,8 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
     if (a.kc > 64 || a.k > a.kc || a.k > 64 || a.dp % 4 != 0 || !a.stats || !a.fail_list)
         return hipErrorInvalidValue;
-    if (a.raw_d && (!a.raw_i || a.raw_km < a.k || a.raw_lists <= 0)) return hipErrorInvalidValue;
+    if (a.raw_d && (!a.raw_i || !a.chance_list || a.raw_km < a.k || a.raw_lists <= 0))
+        return hipErrorInvalidValue;
 #define IMGREC_RERANK(ITV)                                                                          \
     hipLaunchKernelGGL((rerank_certify_kernel<ITV>), dim3((unsigned)a.nq), dim3(kRerankWaves * 64), \
                        0, st, a)
@@ -586,6 +616,10 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     else if (a.dp <= 2048) IMGREC_RERANK(8);
     else IMGREC_RERANK(0);
 #undef IMGREC_RERANK
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !a.raw_d) return e;
+    const unsigned grid = (unsigned)std::min<int64_t>(a.nq, 256);
+    hipLaunchKernelGGL(second_chance_kernel, dim3(grid), dim3(kRerankWaves * 64), 0, st, a);
     return hipGetLastError();
 }
 

@@ -81,7 +81,9 @@ int grow_stats(knn_index* ix, int64_t nq, hipStream_t st) {
         KNN_HIP(hipMemsetAsync(ix->stat, 0, 12 * sizeof(int), st));
         ix->stat_seq = 0;
     }
-    return grow(&ix->fail, &ix->fail_cap, (size_t)nq);
+    int rc = grow(&ix->fail, &ix->fail_cap, (size_t)nq);
+    if (rc != KNN_OK) return rc;
+    return grow(&ix->chance, &ix->chance_cap, (size_t)nq);
 }
 
 // Exact fp32 re-run of the queries this chunk's certificate left (list ix->fail, count in the
@@ -127,6 +129,7 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     const int parity = ix->stat_seq & 1;
     r.stats = ix->stat + 4 * parity;
     r.fail_list = ix->fail;
+    r.chance_list = ix->chance;
     KNN_HIP(launch_rerank_certify(r, st));
     const int rc = run_fallback(ix, qpad, qnorm, nq, k, D, I, st, parity, first);
     if (rc != KNN_OK) {           // the parities may hold this chunk's counts: start clean
