@@ -67,6 +67,9 @@ SIGNATURES = {
     "color_hist_device": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp]),
     "color_hist_host": (_i, [_vp, _i64, _vp, _vp, _i64, _i, _i, _vp, _vp]),
     "color_hist_last_error": (C.c_char_p, []),
+    "color_host_register": (_i, [_vp, _i64]),
+    "color_host_unregister": (_i, [_vp]),
+    "color_hist_batch_async": (_i, [_vp, _i64, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp]),
     # imgrec_ingest.h
     "ingest_parse_f32": (_i64, [_vp, _i64, _vp, _i64]),
     "ingest_concat_rows": (_i64, [C.POINTER(_vp), _pi64, _i64, _i, _pi64, _vp, _vp]),

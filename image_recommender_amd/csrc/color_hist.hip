@@ -336,4 +336,57 @@ int color_hist_host(const uint8_t* pixels, int64_t total_bytes, const int64_t* o
     return rc;
 }
 
+int color_host_register(void* ptr, int64_t bytes) {
+    if (!ptr || bytes <= 0) {
+        set_err("bad host range");
+        return -1;
+    }
+    const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        set_err("hipHostRegister failed: %s", hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
+
+int color_host_unregister(void* ptr) {
+    if (!ptr) return 0;
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) {
+        set_err("hipHostUnregister failed: %s", hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
+
+int color_hist_batch_async(const uint8_t* host_pixels, int64_t bytes, const int64_t* host_meta,
+                           int64_t n, int bins, uint8_t* dev_pixels, int64_t* dev_meta,
+                           float* dev_out, uint32_t* dev_counts, void* stream) {
+    if (n < 0 || bytes < 0 || bins < 1 || bins > COLOR_HIST_MAX_BINS) {
+        set_err("bad arguments (n=%lld bytes=%lld bins=%d)", (long long)n, (long long)bytes, bins);
+        return -1;
+    }
+    if (n == 0) return 0;
+    if (!host_pixels || !host_meta || !dev_pixels || !dev_meta || !dev_out) {
+        set_err("NULL pointer");
+        return -1;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t o = host_meta[i], np = host_meta[n + i];
+        if (o < 0 || np < 0 || o + 3 * np > bytes) {
+            set_err("image %lld lies outside the batch's pixel bytes", (long long)i);
+            return -1;
+        }
+    }
+    const hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemcpyAsync(dev_pixels, host_pixels, (size_t)bytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(dev_meta, host_meta, (size_t)(2 * n) * sizeof(int64_t), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) {
+        set_err("batch upload failed: %s", hipGetErrorString(e));
+        return -2;
+    }
+    return color_hist_device(dev_pixels, dev_meta, dev_meta + n, n, bins, dev_out, dev_counts, stream);
+}
+
 }  // extern "C"

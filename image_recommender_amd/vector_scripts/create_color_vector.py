@@ -3,9 +3,12 @@
 The reference (/root/reference/vector_scripts/create_color_vector.py:12-78) decodes every image
 with OpenCV in a ProcessPoolExecutor and runs cv2.calcHist (16 bins per channel, R|G|B, then L2
 normalisation) per image.  Here a batch of decoded images is packed into one byte buffer and the
-HIP kernel ``color_hist_device`` (csrc/color_hist.hip) computes all histograms in one launch;
-images are decoded with PIL in a thread pool.  Output: one (3*bins,) float32 vector per image,
-None for unreadable images, exactly like ``compute_vectors`` of the reference.
+HIP kernel ``color_hist_device`` (csrc/color_hist.hip) computes all histograms in one launch.
+``compute_vectors`` (the indexer's batch path, reference :54-78) streams files through
+``decode_pipeline.ColorDecodePipeline``: worker processes decode into a page-locked shared-memory
+ring, batches are DMA'd to the GPU and histogrammed while later files decode.  Output: one
+(3*bins,) float32 vector per image, None for unreadable images, exactly like ``compute_vectors``
+of the reference.
 """
 from __future__ import annotations
 
@@ -99,7 +102,23 @@ class ColorVectorIndexer(BaseVectorIndexer):
         return results
 
     def compute_vectors(self, paths: list[str], chunksize=16):
-        return self.compute_paths(paths, self.base_dir, self.bins)
+        from .decode_pipeline import ColorDecodePipeline
+        if getattr(self, "_pipeline", None) is None:
+            self._pipeline = ColorDecodePipeline(bins=self.bins)
+        full = [p if Path(p).is_absolute() else self.base_dir / p for p in paths]
+        res = self._pipeline.histograms(full)
+        for p, v in zip(paths, res):
+            if v is None:
+                print(f"Image unreadable or wrong shape: {p}")
+        return res
+
+    def run(self):
+        try:
+            super().run()
+        finally:
+            if getattr(self, "_pipeline", None) is not None:
+                self._pipeline.close()
+                self._pipeline = None
 
 
 if __name__ == "__main__":

@@ -32,6 +32,20 @@ int color_hist_host(const uint8_t* pixels, int64_t total_bytes, const int64_t* o
                     const int64_t* npix, int64_t n_images, int bins, int device, float* out,
                     uint32_t* counts);
 
+/* Page-lock a host range (hipHostRegister) so hipMemcpyAsync from it is an asynchronous DMA — the
+ * shared-memory slots the decode pipeline's worker processes write decoded images into
+ * (vector_scripts/decode_pipeline.py).  color_host_unregister releases it. */
+int color_host_register(void* ptr, int64_t bytes);
+int color_host_unregister(void* ptr);
+
+/* One decoded batch in a page-locked host slot: `bytes` of pixels and the batch's meta (n image
+ * offsets into the pixels, then n pixel counts, int64) are copied to dev_pixels / dev_meta on
+ * `stream`, then the n histograms are computed into dev_out (and dev_counts when not NULL).
+ * Asynchronous: the slot may be rewritten once the stream has passed this call. */
+int color_hist_batch_async(const uint8_t* host_pixels, int64_t bytes, const int64_t* host_meta,
+                           int64_t n, int bins, uint8_t* dev_pixels, int64_t* dev_meta,
+                           float* dev_out, uint32_t* dev_counts, void* stream);
+
 /* Same error-string convention as knn_last_error(). */
 const char* color_hist_last_error(void);
 
