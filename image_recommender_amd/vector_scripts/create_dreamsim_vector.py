@@ -6,12 +6,36 @@ weights downloaded at run time), embeds batches of 128 images resized to 224x224
 L2-normalises each embedding (:92).  The ensemble is three ViT-B/16 towers — DINO (768-d CLS),
 OpenAI CLIP and OpenCLIP (512-d projected CLS) — concatenated to 1792 dimensions.
 
-This module implements that architecture in plain PyTorch (bf16 autocast, fused
-scaled-dot-product attention — it runs on PyTorch-ROCm, no hand kernel is required for it).
-Pretrained weights cannot be fetched here: ``DreamSimVectorIndexer`` needs ``weights_path`` (a
-state dict for ``DreamSimEnsemble``) and raises like the reference does when the model cannot be
-loaded; ``allow_random_init=True`` builds a randomly initialised model for throughput
-measurements only (its embeddings are not DreamSim embeddings).
+This module implements that architecture in plain PyTorch (bf16 matrix products with fp32
+LayerNorm / residual stream, fused scaled-dot-product attention — it runs on PyTorch-ROCm, no hand
+kernel is required for it).  Pretrained weights cannot be fetched here: ``DreamSimVectorIndexer``
+needs ``weights_path`` and raises like the reference does when the model cannot be loaded;
+``allow_random_init=True`` builds a randomly initialised model for throughput measurements only
+(its embeddings are not DreamSim embeddings; embedding parity is unpinned).
+
+Weights: ``weights_path`` holds either a state dict of ``DreamSimEnsemble`` (keys below) or the
+three towers' own checkpoints, converted by ``ensemble_state_from_towers``:
+
+=====================================  ==========================================================
+ours (``towers.{t}.`` prefix)          source layout
+=====================================  ==========================================================
+``patch.weight`` / ``patch.bias``      DINO ``patch_embed.proj.*``; CLIP / OpenCLIP ``conv1.weight``
+``cls`` (1, 1, 768)                    DINO ``cls_token``; CLIP ``class_embedding`` (768,)
+``pos`` (1, 197, 768)                  DINO ``pos_embed``; CLIP ``positional_embedding`` (197, 768)
+``ln_pre.*``                           CLIP ``ln_pre.*`` (DINO has none)
+``blocks.{i}.ln1.*`` / ``ln2.*``       DINO ``blocks.{i}.norm1/norm2``; CLIP ``transformer.resblocks.{i}.ln_1/ln_2``
+``blocks.{i}.qkv.*``                   DINO ``blocks.{i}.attn.qkv``; CLIP ``...attn.in_proj_weight/bias`` (q|k|v rows)
+``blocks.{i}.proj.*``                  DINO ``blocks.{i}.attn.proj``; CLIP ``...attn.out_proj``
+``blocks.{i}.fc1.*`` / ``fc2.*``       DINO ``blocks.{i}.mlp.fc1/fc2``; CLIP ``...mlp.c_fc/c_proj``
+``ln_post.*``                          DINO ``norm``; CLIP ``ln_post``
+``head.weight`` (512, 768)             CLIP ``proj`` (768, 512) transposed (DINO: none, CLS is the feature)
+=====================================  ==========================================================
+
+(t = 0 dino_vitb16 [timm / facebookresearch-dino names], 1 OpenAI clip_vitb16 visual, 2
+open_clip_vitb16 visual; a ``visual.`` prefix is stripped.)  DreamSim's own fine-tuning ships
+LoRA adapters for these towers; merged into the base weights (W + scale * B @ A) they are plain
+weights of this layout.  tests/test_dreamsim_cpu.py checks the conversion against independent
+forwards written in each source layout's own module structure.
 """
 from __future__ import annotations
 
@@ -36,7 +60,17 @@ def _torch():
     return torch, nn, F
 
 
-def build_ensemble(seed: int | None = 0):
+def _lin(m, x):
+    """A Linear / projection through its cached low-precision copy when prepared (see
+    prepare_inference), else as is."""
+    w = getattr(m, "w_lp", None)
+    if w is None:
+        return m(x)
+    F = _torch()[2]
+    return F.linear(x.to(w.dtype), w, m.b_lp)
+
+
+def build_ensemble(seed: int | None = 0, depth: int = 12):
     torch, nn, F = _torch()
 
     class Block(nn.Module):
@@ -53,25 +87,25 @@ def build_ensemble(seed: int | None = 0):
 
         def forward(self, x):
             b, n, c = x.shape
-            qkv = self.qkv(self.ln1(x)).view(b, n, 3, self.heads, c // self.heads)
+            qkv = _lin(self.qkv, self.ln1(x)).view(b, n, 3, self.heads, c // self.heads)
             q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
             a = F.scaled_dot_product_attention(q, k, v)
-            x = x + self.proj(a.transpose(1, 2).reshape(b, n, c))
-            h = self.fc1(self.ln2(x))
+            x = x + _lin(self.proj, a.transpose(1, 2).reshape(b, n, c))
+            h = _lin(self.fc1, self.ln2(x))
             h = h * torch.sigmoid(1.702 * h) if self.quick_gelu else F.gelu(h)
-            return x + self.fc2(h)
+            return x + _lin(self.fc2, h)
 
     class ViT(nn.Module):
         """ViT-B/16 tower; `out_dim` adds a CLIP-style projection of the CLS token."""
 
-        def __init__(self, kind, out_dim=None, depth=12, dim=768, patch=16, img=224):
+        def __init__(self, kind, out_dim=None, blocks=12, dim=768, patch=16, img=224):
             super().__init__()
             self.kind = kind
             self.patch = nn.Conv2d(3, dim, patch, patch, bias=(kind == "dino"))
             self.cls = nn.Parameter(torch.zeros(1, 1, dim))
             self.pos = nn.Parameter(torch.zeros(1, (img // patch) ** 2 + 1, dim))
             self.ln_pre = nn.LayerNorm(dim) if kind != "dino" else nn.Identity()
-            self.blocks = nn.ModuleList(Block(dim, quick_gelu=(kind == "clip")) for _ in range(depth))
+            self.blocks = nn.ModuleList(Block(dim, quick_gelu=(kind == "clip")) for _ in range(blocks))
             self.ln_post = nn.LayerNorm(dim)
             self.head = nn.Linear(dim, out_dim, bias=False) if out_dim else nn.Identity()
             mean, std = _MEAN_STD[kind]
@@ -82,19 +116,31 @@ def build_ensemble(seed: int | None = 0):
 
         def forward(self, x):                      # x: (B, 3, 224, 224) in [0, 1]
             x = (x - self.mean) / self.std
-            x = self.patch(x).flatten(2).transpose(1, 2)
+            w = getattr(self.patch, "w_lp", None)
+            if w is None:
+                x = self.patch(x).flatten(2).transpose(1, 2)
+            else:
+                # the stride-16 16x16 patch conv as ONE matrix product: (B*196, 3*16*16) x (768,
+                # 768)^T, patches laid out (c, kh, kw) like the conv weight
+                b, c, hh, ww = x.shape
+                p = self.patch.kernel_size[0]
+                x = x.to(w.dtype).reshape(b, c, hh // p, p, ww // p, p).permute(0, 2, 4, 1, 3, 5)
+                x = F.linear(x.reshape(b, (hh // p) * (ww // p), c * p * p), w, self.patch.b_lp)
+                x = x.float()
             x = torch.cat([self.cls.expand(x.shape[0], -1, -1), x], 1) + self.pos
             x = self.ln_pre(x)
             for blk in self.blocks:
                 x = blk(x)
-            return self.head(self.ln_post(x[:, 0]))
+            x = self.ln_post(x[:, 0])
+            return x if isinstance(self.head, nn.Identity) else _lin(self.head, x)
 
     class DreamSimEnsemble(nn.Module):
         """dino_vitb16 (768) | clip_vitb16 (512) | open_clip_vitb16 (512) -> 1792."""
 
         def __init__(self):
             super().__init__()
-            self.towers = nn.ModuleList([ViT("dino"), ViT("clip", 512), ViT("open_clip", 512)])
+            self.towers = nn.ModuleList([ViT("dino", blocks=depth), ViT("clip", 512, blocks=depth),
+                                         ViT("open_clip", 512, blocks=depth)])
 
         @property
         def dim(self):
@@ -104,9 +150,68 @@ def build_ensemble(seed: int | None = 0):
             parts = [F.normalize(t(x).float(), dim=-1) for t in self.towers]
             return torch.cat(parts, -1)
 
+        def prepare_inference(self, dtype):
+            """Cache low-precision copies of every matrix-product weight once (autocast would
+            re-cast them on every forward); LayerNorms and the residual stream stay fp32."""
+            for m in self.modules():
+                if isinstance(m, (nn.Linear, nn.Conv2d)):
+                    w = m.weight.detach()
+                    m.w_lp = (w.reshape(w.shape[0], -1) if w.dim() > 2 else w).to(dtype).contiguous()
+                    m.b_lp = m.bias.detach().to(dtype) if m.bias is not None else None
+            return self
+
     if seed is not None:
         torch.manual_seed(seed)
     return DreamSimEnsemble()
+
+
+def ensemble_state_from_towers(dino: dict, clip: dict, open_clip: dict) -> dict:
+    """State dict of DreamSimEnsemble from the three towers' own checkpoints (layouts in the module
+    docstring): DINO ViT-B/16 (timm / facebookresearch-dino names) and the ``visual`` parts of the
+    OpenAI CLIP and OpenCLIP ViT-B/16 models (LoRA already merged)."""
+    out = {}
+
+    def strip(sd):
+        return {(k[7:] if k.startswith("visual.") else k): v for k, v in sd.items()}
+
+    d = strip(dino)
+    pre = "towers.0."
+    out[pre + "patch.weight"] = d["patch_embed.proj.weight"]
+    out[pre + "patch.bias"] = d["patch_embed.proj.bias"]
+    out[pre + "cls"] = d["cls_token"].reshape(1, 1, -1)
+    out[pre + "pos"] = d["pos_embed"].reshape(1, -1, d["pos_embed"].shape[-1])
+    nb = 1 + max(int(k.split(".")[1]) for k in d if k.startswith("blocks."))
+    for i in range(nb):
+        s_, o_ = f"blocks.{i}.", f"{pre}blocks.{i}."
+        for a, b in (("norm1", "ln1"), ("norm2", "ln2"), ("attn.qkv", "qkv"), ("attn.proj", "proj"),
+                     ("mlp.fc1", "fc1"), ("mlp.fc2", "fc2")):
+            out[o_ + b + ".weight"] = d[s_ + a + ".weight"]
+            out[o_ + b + ".bias"] = d[s_ + a + ".bias"]
+    out[pre + "ln_post.weight"] = d["norm.weight"]
+    out[pre + "ln_post.bias"] = d["norm.bias"]
+    for t, sd in ((1, clip), (2, open_clip)):
+        c = strip(sd)
+        pre = f"towers.{t}."
+        out[pre + "patch.weight"] = c["conv1.weight"]
+        out[pre + "cls"] = c["class_embedding"].reshape(1, 1, -1)
+        out[pre + "pos"] = c["positional_embedding"].reshape(1, *c["positional_embedding"].shape)
+        out[pre + "ln_pre.weight"] = c["ln_pre.weight"]
+        out[pre + "ln_pre.bias"] = c["ln_pre.bias"]
+        nb = 1 + max(int(k.split(".")[2]) for k in c if k.startswith("transformer.resblocks."))
+        for i in range(nb):
+            s_, o_ = f"transformer.resblocks.{i}.", f"{pre}blocks.{i}."
+            out[o_ + "ln1.weight"], out[o_ + "ln1.bias"] = c[s_ + "ln_1.weight"], c[s_ + "ln_1.bias"]
+            out[o_ + "ln2.weight"], out[o_ + "ln2.bias"] = c[s_ + "ln_2.weight"], c[s_ + "ln_2.bias"]
+            out[o_ + "qkv.weight"] = c[s_ + "attn.in_proj_weight"]
+            out[o_ + "qkv.bias"] = c[s_ + "attn.in_proj_bias"]
+            out[o_ + "proj.weight"] = c[s_ + "attn.out_proj.weight"]
+            out[o_ + "proj.bias"] = c[s_ + "attn.out_proj.bias"]
+            out[o_ + "fc1.weight"], out[o_ + "fc1.bias"] = c[s_ + "mlp.c_fc.weight"], c[s_ + "mlp.c_fc.bias"]
+            out[o_ + "fc2.weight"], out[o_ + "fc2.bias"] = c[s_ + "mlp.c_proj.weight"], c[s_ + "mlp.c_proj.bias"]
+        out[pre + "ln_post.weight"] = c["ln_post.weight"]
+        out[pre + "ln_post.bias"] = c["ln_post.bias"]
+        out[pre + "head.weight"] = c["proj"].t().contiguous()
+    return out
 
 
 class DreamSimVectorIndexer(BaseVectorIndexer):
@@ -130,19 +235,25 @@ class DreamSimVectorIndexer(BaseVectorIndexer):
         model = build_ensemble(seed=0)
         if weights_path:
             state = torch.load(weights_path, map_location="cpu", weights_only=True)
+            if {"dino", "clip", "open_clip"} <= set(state):       # the towers' own checkpoints
+                state = ensemble_state_from_towers(state["dino"], state["clip"], state["open_clip"])
             model.load_state_dict(state)
         elif not allow_random_init:
             raise RuntimeError("DreamSim ensemble weights are not available (the reference "
                                "downloads them at run time; pass weights_path=...)")
         self.model = model.to(self.device).eval()
+        if self.device.type == "cuda":
+            self.model.prepare_inference(torch.bfloat16)
         self.dim = model.dim
         self._log_and_print("DreamSim model loaded and warmed up.", level="info")
 
     def embed_tensor(self, images):
-        """(B, 3, 224, 224) float tensor in [0, 1] on the model device -> (B, 1792) normalised."""
+        """(B, 3, 224, 224) float tensor in [0, 1] on the model device -> (B, 1792) normalised.
+        On the GPU the matrix products run in bf16 from weights cast once (prepare_inference),
+        LayerNorm and the residual stream in fp32 — what autocast does, without re-casting every
+        weight on every forward."""
         torch, _, F = _torch()
-        with torch.no_grad(), torch.autocast(device_type=self.device.type, dtype=torch.bfloat16,
-                                             enabled=self.device.type == "cuda"):
+        with torch.no_grad():
             emb = self.model.embed(images)
         return F.normalize(emb.float(), dim=-1)
 
