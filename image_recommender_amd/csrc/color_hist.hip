@@ -123,16 +123,6 @@ __device__ __forceinline__ void count_granule(uint32_t* __restrict__ col, const 
 template <int BINS, int P0>
 __device__ __forceinline__ void count_body(uint32_t* __restrict__ col, const uint4* __restrict__ vb,
                                            int64_t ngran, int tid) {
-#ifdef IMGREC_COLOR_NO_PIPE
-    int64_t g = tid;
-    for (; g + NT < ngran; g += 2 * NT) {               // two granules in flight per lane
-        const uint4 a0 = vb[3 * g], b0 = vb[3 * g + 1], c0 = vb[3 * g + 2];
-        const uint4 a1 = vb[3 * (g + NT)], b1 = vb[3 * (g + NT) + 1], c1 = vb[3 * (g + NT) + 2];
-        count_granule<BINS, P0>(col, a0, b0, c0);
-        count_granule<BINS, P0>(col, a1, b1, c1);
-    }
-    if (g < ngran) count_granule<BINS, P0>(col, vb[3 * g], vb[3 * g + 1], vb[3 * g + 2]);
-#else
     // software pipeline: the loads of granule g + NT are in flight while granule g is counted
     int64_t g = tid;
     if (g >= ngran) return;
@@ -144,7 +134,6 @@ __device__ __forceinline__ void count_body(uint32_t* __restrict__ col, const uin
         a = an; b = bn; c = cn;
     }
     count_granule<BINS, P0>(col, a, b, c);
-#endif
 }
 
 template <int BINS>
@@ -255,7 +244,6 @@ int color_hist_device(const uint8_t* pixels, const int64_t* offsets, const int64
         set_err("NULL pointer");
         return -1;
     }
-#ifndef IMGREC_COLOR_GENERIC_ONLY
     if (bins == 16) {
         hipLaunchKernelGGL(color_hist_fixed_kernel<16>, dim3((unsigned)n_images), dim3(NT), 0,
                            (hipStream_t)stream, pixels, offsets, npix, out, counts);
@@ -266,7 +254,6 @@ int color_hist_device(const uint8_t* pixels, const int64_t* offsets, const int64
         }
         return 0;
     }
-#endif
     const size_t lds = (size_t)3 * bins * NT * sizeof(uint32_t);
     hipLaunchKernelGGL(color_hist_kernel, dim3((unsigned)n_images), dim3(NT), lds,
                        (hipStream_t)stream, pixels, offsets, npix, bins, out, counts);

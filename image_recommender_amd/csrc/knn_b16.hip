@@ -47,21 +47,8 @@
 #include "knn_kernels.h"
 
 // Stage depth in 32-bit words per staged row (32 = 64 bf16 per row and stage).
-#ifndef IMGREC_B16_BKW
-#define IMGREC_B16_BKW 32
-#endif
-#ifndef IMGREC_B16_QB_PER_XCD      // query blocks per XCD group (see the block map)
-#define IMGREC_B16_QB_PER_XCD 4
-#endif
 
 namespace imgrec {
-#ifdef IMGREC_B16_PROF
-// Debug build only (tools/prof_b16.py): per-wave cycle and event counts, summed over waves.
-__device__ unsigned long long g_b16prof[8];
-#define B16_T(v) const unsigned long long v = __builtin_readcyclecounter()
-#else
-#define B16_T(v)
-#endif
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -72,7 +59,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kNW = 8;                    // waves: 2 along rows x 4 along queries
 constexpr int kBM = kB16BigRows;          // 256 corpus rows per tile
 constexpr int kBQ = kB16BigQueries;       // 256 queries per workgroup
-constexpr int kBKW = IMGREC_B16_BKW;      // 32-bit words (2 bf16) per staged row
+constexpr int kBKW = 32;                  // 32-bit words (2 bf16) per staged row
 constexpr int kNS = 2;                    // stages in the LDS ring
 constexpr int kRowB = kBKW * 4;           // bytes per staged row
 constexpr int kCPR = kBKW / 4;            // 16-B chunks per staged row
@@ -152,12 +139,8 @@ __device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float 
     for (int p = 0; p < K; ++p) c[p] = d < kd[p];
 #pragma unroll
     for (int p = K - 1; p > 0; --p) {
-#ifdef IMGREC_NO_MED3
-        kd[p] = c[p - 1] ? kd[p - 1] : (c[p] ? d : kd[p]);
-#else
         // the same select on an ascending list is the median of (kd[p-1], d, kd[p]): one v_med3
         kd[p] = __builtin_amdgcn_fmed3f(kd[p - 1], d, kd[p]);
-#endif
         ki[p] = c[p - 1] ? ki[p - 1] : (c[p] ? id : ki[p]);
     }
     kd[0] = c[0] ? d : kd[0];
@@ -201,7 +184,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
     // G query blocks per row split group on one XCD (G = nqb: all query blocks of a split share
     // its corpus tiles through that XCD's L2; smaller G keeps fewer query blocks per L2)
-    constexpr int kG = IMGREC_B16_QB_PER_XCD;
+    constexpr int kG = 4;                   // query blocks per XCD group
     const int G = (nqb % kG == 0) ? kG : nqb;
     const int qbg = wgid / (nsplit * G), rem = wgid - qbg * (nsplit * G);
     const int split = rem / G;
@@ -231,11 +214,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     // DMA pieces of this wave: kLPW consecutive pieces of the A tile (waves 0-3) or B tile (4-7);
     // lane -> (row prow of the piece, chunk pchk), source chunk pre-swizzled.
     const bool isA = wave < 4;
-#ifndef IMGREC_B16_NO_PRIO
     // waves 4-7 (the younger half) lose issue arbitration to 0-3 at every segment start; a static
     // raised priority evens that out (~1 %; per-cluster priority flips measured slower)
     if (!isA) __builtin_amdgcn_s_setprio(1);
-#endif
     const int pbase = (isA ? wave : wave - 4) * kLPW;          // first piece index in its tile
     const int prow = lane / kCPR, pchk = lane % kCPR;
     // Per-piece lane offsets in bytes from the stage's scalar base (the tile's first row, or the
@@ -337,14 +318,6 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         for (int h = 0; h < 2; ++h) fb[h] = *reinterpret_cast<const u32x4*>(sb + aoff[c] + boff + h * 32 * kRowB);
     };
     auto mfma_step = [&](f32x16 (&acc)[4][2], const u32x4 (&fa)[4], const u32x4 (&fb)[2]) __attribute__((always_inline)) {
-#ifdef IMGREC_ABLATE_NO_MFMA
-        // ablation: fragments read and consumed, no matrix work
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) asm volatile("" ::"v"(fa[rb]));
-#pragma unroll
-        for (int h = 0; h < 2; ++h) asm volatile("" ::"v"(fb[h]));
-        if (nq < 0)
-#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -366,12 +339,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         if (total > 1) issue(1);
         read_frags(smem, 0, fa[0], fb[0]);
     }
-#ifdef IMGREC_B16_PROF
-    unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    B16_T(tk0);
-#endif
     for (int t = t0; t < t1; ++t) {
-        B16_T(tl0);
         f32x16 acc[4][2];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
@@ -386,28 +354,16 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             }
             // (the fences keep the compiler from sinking k-step kKS-2's MFMAs below the wait)
             __builtin_amdgcn_sched_barrier(0);
-#ifdef IMGREC_ABLATE_NO_WAIT
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
             __builtin_amdgcn_sched_barrier(0);
             barrier_lds();
             __builtin_amdgcn_sched_barrier(0);
             // (after a tile's last stage the next fragments are read after the epilogue instead)
             if (s + 1 < nst) read_frags(smem + ((g + 1) & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
-#ifdef IMGREC_ABLATE_NO_DMA
-            if (g + 2 < total && (g + 2) % nst == 0) issue(g + 2);   // ablation: norms + a stage per tile
-#else
             if (g + 2 < total) issue(g + 2);
-#endif
             mfma_step(acc, fa[(kKS - 1) & 1], fb[(kKS - 1) & 1]);
         }
         // ---- epilogue of tile t (see above)
-        B16_T(te0);
-#ifdef IMGREC_B16_PROF
-        pr[5] += te0 - tl0;
-#endif
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
@@ -415,11 +371,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         float other[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-#ifdef IMGREC_ABLATE_NO_SHARE
-            other[h] = INFINITY;
-#else
             other[h] = share[(((1 - wr) * 4 + wq) * 2 + h) * 32 + li];
-#endif
         }
         float cth[2];
         auto screen = [&]() __attribute__((always_inline)) {
@@ -435,15 +387,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         screen();
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-#ifdef IMGREC_ABLATE_NO_EPILOGUE
-            asm volatile("" ::"v"(acc[rb][0]), "v"(acc[rb][1]));
-            continue;
-#endif
-#ifndef IMGREC_B16_SCREEN_ONCE
             // re-tighten after the previous block's insertions (in the first tile the empty lists
             // would otherwise pass every row of all four blocks)
             if (rb > 0) screen();
-#endif
             const int rbase = wr * 128 + rb * 32 + 4 * lh;      // tile row of accumulator reg 0
             unsigned live = 0xffffu;                            // rows of the block that count
             if (!full) {
@@ -472,14 +418,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const unsigned m = msk[h] & live;
-#ifdef IMGREC_ABLATE_SCREEN_ONLY
-                asm volatile("" ::"v"(m));
-                continue;
-#endif
                 if (!__any(m != 0)) continue;
-#ifdef IMGREC_B16_PROF
-                pr[6] += t == t0 ? 0 : 1;
-#endif
                 auto key_of = [&](float a, int tr) __attribute__((always_inline)) {
                     float kv;
                     if (L2) {
@@ -499,9 +438,6 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     park[64 + lane] = make_float4(acc[rb][h][8 * hf + 4], acc[rb][h][8 * hf + 5],
                                                   acc[rb][h][8 * hf + 6], acc[rb][h][8 * hf + 7]);
                     while (__any(mh != 0)) {
-#ifdef IMGREC_B16_PROF
-                        pr[t == t0 ? 3 : 4] += 1;
-#endif
                         if (mh) {
                             const int r8 = __builtin_ctz(mh);
                             mh &= mh - 1u;
@@ -522,23 +458,8 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
             if (lh == 0) share[((wr * 4 + wq) * 2 + h) * 32 + li] = jb;
         }
-#ifdef IMGREC_B16_PROF
-        {
-            B16_T(te1);
-            pr[t == t0 ? 0 : 1] += te1 - te0;
-            pr[7] += 1;
-        }
-#endif
         if (g < total) read_frags(smem + (g & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
     }
-#ifdef IMGREC_B16_PROF
-    {
-        B16_T(tk1);
-        pr[2] = tk1 - tk0;
-        if (lane == 0)
-            for (int i = 0; i < 8; ++i) atomicAdd(&g_b16prof[i], pr[i]);
-    }
-#endif
 
     // ---- one list per (query, row split): fold the partner lane's list (lane ^ 32, the query's
     // other rows) by shuffles, then wave wr = 1's lists into wave wr = 0's through LDS.  Entries a
@@ -610,12 +531,3 @@ hipError_t launch_b16_big(const TileArgs& a, hipStream_t st) {
 
 }  // namespace imgrec
 
-#ifdef IMGREC_B16_PROF
-extern "C" int knn_debug_b16prof(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(imgrec::g_b16prof), 8 * sizeof(unsigned long long)) !=
-        hipSuccess)
-        return -2;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(imgrec::g_b16prof), z, sizeof(z)) == hipSuccess ? 0 : -2;
-}
-#endif

@@ -34,16 +34,6 @@
 
 namespace imgrec {
 
-#ifdef IMGREC_PROF
-// Debug build only: per-phase s_memtime cycle totals of the fused kernel, summed over waves.
-__device__ unsigned long long g_prof[8];
-#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define PROF_ADD(i, d) prof[i] += (d)
-#else
-#define PROF_T(v)
-#define PROF_ADD(i, d)
-#endif
-
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -218,12 +208,8 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
     for (int p = 0; p < K; ++p) c[p] = d < kd[p];
 #pragma unroll
     for (int p = K - 1; p > 0; --p) {
-#ifdef IMGREC_NO_MED3
-        kd[p] = c[p - 1] ? kd[p - 1] : (c[p] ? d : kd[p]);
-#else
         // the same select on an ascending list is the median of (kd[p-1], d, kd[p]): one v_med3
         kd[p] = __builtin_amdgcn_fmed3f(kd[p - 1], d, kd[p]);
-#endif
         ki[p] = c[p - 1] ? ki[p - 1] : (c[p] ? id : ki[p]);
     }
     kd[0] = c[0] ? d : kd[0];
@@ -231,11 +217,7 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
 }
 
 // 4-wave workgroups run two per CU (two waves per SIMD): hold them to 256 VGPR+AGPR per lane.
-#ifdef IMGREC_ABLATE_NO_WAVES_HINT
-#define IMGREC_MIN_WAVES(nw) 1
-#else
 #define IMGREC_MIN_WAVES(nw) ((nw) == 4 ? 2 : 1)
-#endif
 template <int WR, int WQ, int KM, int NS, int BK, int MODE, int WB>
 __global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
 knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
@@ -318,11 +300,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     for (int j = 0; j < LPW; ++j) {
         const int pc = wave * LPW + j;
         pis_a[j] = pc < PA;
-#ifdef IMGREC_NO_NT
-        pnt[j] = false;
-#else
         pnt[j] = MODE == kModeBF16 && pis_a[j] && nqb == 1;   // fp32 rows: 1.94 -> 2.70 ms at nq = 1
-#endif
         const int prow0 = pis_a[j] ? pc * RPP : (pc - PA) * RPP;
         poff[j] = (int64_t)prow0 * dp + (((prow0 / RPP) & 1) ? goff1 : goff0);
         pdst[j] = (uint32_t)(pis_a[j] ? pc * 256 : SA + (pc - PA) * 256) * 4u;
@@ -342,9 +320,6 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
         const int k0 = is * BK;
 #pragma unroll
         for (int j = 0; j < LPW; ++j) {
-#ifdef IMGREC_ABLATE_A_ONLY
-            if (pis_a[j])
-#endif
             if (pnt[j]) dma16_nt(itile + poff[j] + k0, st + pdst[j]);
             else dma16((pis_a[j] ? itile : qbase) + poff[j] + k0, st + pdst[j]);
         }
@@ -357,10 +332,6 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     int remaining = (t1 - t0) * nsteps;     // stages not yet consumed
     int cbuf = 0;
 
-#ifdef IMGREC_PROF
-    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    PROF_T(tk0);
-#endif
     for (int t = t0; t < t1; ++t) {
         const int row0 = tile(t) * BM;
         f32x16 acc[WB];
@@ -370,18 +341,11 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
         const float* st = smem;
         for (int s = 0; s < nsteps; ++s) {
             // own DMA of this stage landed (later stages may stay in flight)
-            PROF_T(ta);
             --remaining;                             // stages issued after this one: min(NS-2, remaining)
-#ifdef IMGREC_ABLATE_NO_WAIT
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
             if (remaining >= NS - 2) wait_vmcnt<LPW * (NS - 2)>();
             else if (NS > 3 && remaining == 1) wait_vmcnt<LPW>();
             else wait_vmcnt<0>();
-#endif
-            PROF_T(tb);
             barrier_raw();                           // everyone's DMA landed; previous stage read
-            PROF_T(tc);
 
             st = smem + cbuf * STAGE;
             cbuf = (cbuf + 1 == NS) ? 0 : cbuf + 1;
@@ -407,10 +371,7 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
             // overlaps the LDS latency), before the MFMAs.  Measured alternatives, all slower:
             // pieces pinned between MFMAs (38.6 ms vs 33.5 at BK=16), staggered per wave (38.8),
             // a 5-deep ring (39.0).
-#ifndef IMGREC_ABLATE_NO_DMA
             issue_next();                            // refills the buffer the previous stage used
-#endif
-            PROF_T(td);
             if constexpr (MODE == kModeBF16) {
                 // bf16 rows (2 elements per 32-bit word): this lane half's chunk c holds the 8
                 // elements of MFMA k-step c (depth 32h + 8c + 0..7 of the 64-deep stage, the same
@@ -446,10 +407,6 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                         acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][kk], bq[kk], acc[b], 0, 0, 0);
                 }
             }
-#ifdef IMGREC_PROF
-            PROF_T(te);
-            PROF_ADD(0, tb - ta); PROF_ADD(1, tc - tb); PROF_ADD(2, td - tc); PROF_ADD(3, te - td);
-#endif
         }
 
         // ---- epilogue: key = L2 distance (faiss exhaustive_L2sqr_blas form, clamped at 0) or
@@ -459,15 +416,9 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
         // (refilled only after the next barrier, which every wave reaches after its epilogue)
         // and inserted one by one.
         // every wave (all lanes: qvalid is per lane) passes this barrier exactly once per tile
-        PROF_T(tf);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         barrier_raw();                               // all fragment reads of the spent stage done
-        PROF_T(tg);
-#ifdef IMGREC_ABLATE_NO_EPILOGUE
-        if (qvalid && row0 < 0) {   // never taken: keeps the accumulators live, no top-k work
-#else
         if (qvalid) {
-#endif
             const float* nrm = norm_base + ((t - t0) % NS) * BM;
             float* park = const_cast<float*>(st) + wave * (PR * 64);
 #pragma unroll
@@ -520,18 +471,8 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
                 }
             }
         }
-#ifdef IMGREC_PROF
-        PROF_T(th);
-        PROF_ADD(4, tg - tf); PROF_ADD(5, th - tg);
-#endif
     }
 
-#ifdef IMGREC_PROF
-    PROF_T(tk1);
-    prof[6] = tk1 - tk0;
-    if (lane == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd(&g_prof[i], prof[i]);
-#endif
     if (qvalid) {
         const size_t base = (size_t)qcol * ncand + (size_t)((split * WR + wr) * 2 + lh) * KM;
 #pragma unroll
@@ -738,12 +679,8 @@ static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-#ifndef IMGREC_BK_BIG
-#define IMGREC_BK_BIG 32
-#endif
-#ifndef IMGREC_NS_BIG
-#define IMGREC_NS_BIG 3
-#endif
+// (1,8) exact tile of the ablations kept in DESIGN.md: 32-deep stages, 3-slot ring
+constexpr int kBKBig = 32, kNSBig = 3;
 
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
     if (a.mode == kModeBF16) {
@@ -765,9 +702,9 @@ hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st) {
             return launch_tile_km<1, 4, kSplitNS, kSplitBK, kModeSplit, kSplitWB>(a.km, a, st);
         return hipErrorInvalidValue;
     }
-    if (a.dp % IMGREC_BK_BIG != 0 && a.wr == 1 && a.wq == 8)
+    if (a.dp % kBKBig != 0 && a.wr == 1 && a.wq == 8)
         return launch_tile_km<1, 8, 4, 16>(a.km, a, st);
-    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, IMGREC_NS_BIG, IMGREC_BK_BIG>(a.km, a, st);
+    if (a.wr == 1 && a.wq == 8) return launch_tile_km<1, 8, kNSBig, kBKBig>(a.km, a, st);
     if (a.wr == 1 && a.wq == 4 && a.dp % 32 == 0) return launch_tile_km<1, 4, 2, 32>(a.km, a, st);
     if (a.wr == 1 && a.wq == 4) return launch_tile_km<1, 4, 2, 16>(a.km, a, st);
     if (a.wr == 2 && a.wq == 2) return launch_tile_km<2, 2, 3, 16>(a.km, a, st);
@@ -1064,13 +1001,3 @@ hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStr
 
 }  // namespace imgrec
 
-#ifdef IMGREC_PROF
-// Debug build only (tools/prof_phases.py): read and clear the fused kernel's phase counters.
-extern "C" int knn_debug_prof(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(imgrec::g_prof), 8 * sizeof(unsigned long long)) !=
-        hipSuccess)
-        return -2;
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(imgrec::g_prof), z, sizeof(z)) == hipSuccess ? 0 : -2;
-}
-#endif
