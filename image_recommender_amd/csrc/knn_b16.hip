@@ -263,13 +263,17 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
     const int total = (t1 - t0) * nst;
     const uint32_t* qblk = qh + (size_t)qb * kBQ * dw;
 
-    // DMA of stage g into ring slot g % kNS (+ the tile's row norms with its first stage)
+    // DMA of stage g into ring slot g % kNS (+ the tile's row norms with its first stage).  Called
+    // for g = 0, 1, 2, ... in order, so the source is a cursor advanced per stage and moved to the
+    // next tile's first row once per tile (no per-stage division by the stage count: the scalar
+    // address work sits between the barrier and the last k-step's MFMAs).
+    int c_it = t0, c_is = 0;
+    const uint32_t* c_tile = isA ? xh + (size_t)trow(t0, 0) * dw : qblk;
+    int c_ng = (isA && t0 == t1 - 1) ? cnt - t0 * kGPT : kGPT;           // groups in the tile
     auto issue = [&](int g) __attribute__((always_inline)) {
-        const int it = t0 + g / nst, is = g - (g / nst) * nst;
-        const uint32_t* src = (isA ? xh + (size_t)trow(it, 0) * dw : qblk) + is * kBKW;
-        const uint32_t dst = smem0 + (uint32_t)((g % kNS) * kStage) + pdst;
-        const int ng = (isA && it == t1 - 1) ? cnt - it * kGPT : kGPT;   // groups in the tile
-        if (pbase + kLPW <= ng || !isA) {
+        const uint32_t* src = c_tile + c_is * kBKW;
+        const uint32_t dst = smem0 + (uint32_t)((g & (kNS - 1)) * kStage) + pdst;
+        if (pbase + kLPW <= c_ng || !isA) {
 #pragma unroll
             for (int h = 0; h < kLPW / 4; ++h)
                 dma4x(src, dst + 4096u * h, voff_of(4 * h), voff_of(4 * h + 1), voff_of(4 * h + 2),
@@ -279,7 +283,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             // keep stale data; the epilogue masks those rows)
 #pragma unroll
             for (int j = 0; j < kLPW; ++j)
-                if (pbase + j < ng) {
+                if (pbase + j < c_ng) {
                     const uint32_t d = dst + 4096u * (j / 4);
                     switch (j & 3) {                            // constant once unrolled
                         case 0: dma1<0>(src, d, voff_of(j)); break;
@@ -289,10 +293,19 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     }
                 }
         }
-        if (is == 0 && wave < 4)
-            dma4_norm(xnorm + trow(it, wave * 64 + lane),
-                      smem0 + (uint32_t)(kNormOff + ((it - t0) % kNormSlots) * kBM * 4 + wave * 256));
+        if (c_is == 0 && wave < 4)
+            dma4_norm(xnorm + trow(c_it, wave * 64 + lane),
+                      smem0 + (uint32_t)(kNormOff + ((c_it - t0) & (kNormSlots - 1)) * kBM * 4 + wave * 256));
+        if (++c_is == nst) {
+            c_is = 0;
+            ++c_it;
+            if (isA) {
+                c_tile = xh + (size_t)trow(c_it, 0) * dw;
+                c_ng = c_it == t1 - 1 ? cnt - c_it * kGPT : kGPT;
+            }
+        }
     };
+    static_assert(kNS == 2 && kNormSlots == 4, "power-of-two ring slots");
 
     // ---- top-k epilogue of one tile.  Screen: a row can only matter if its key beats T = min(own
     // K-th, the partner lane's K-th, max over the query's four lists of their J-th best) — four
@@ -328,6 +341,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 
     u32x4 fa[2][4], fb[2][2];
     int g = 0;
+    int pend = -1;
     // ---- main loop.  One barrier per stage, placed before the stage's last k-step: by then every
     // wave has read the whole stage (its slot is refilled with stage g + 2 right after) and waited
     // for its own DMA of stage g + 1, so the next stage's first fragments are read after the
@@ -351,6 +365,14 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             for (int c = 0; c + 1 < kKS; ++c) {
                 read_frags(sb, c + 1, fa[(c + 1) & 1], fb[(c + 1) & 1]);
                 mfma_step(acc, fa[c & 1], fb[c & 1]);
+#ifndef IMGREC_B16_NO_STAGGER
+                if (c == 0 && pend >= 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    issue(pend);
+                    pend = -1;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#endif
             }
             // (the fences keep the compiler from sinking k-step kKS-2's MFMAs below the wait)
             __builtin_amdgcn_sched_barrier(0);
@@ -360,7 +382,14 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             __builtin_amdgcn_sched_barrier(0);
             // (after a tile's last stage the next fragments are read after the epilogue instead)
             if (s + 1 < nst) read_frags(smem + ((g + 1) & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
+#ifndef IMGREC_B16_NO_STAGGER
+            if (g + 2 < total) {
+                if (isA) issue(g + 2);
+                else pend = g + 2;
+            }
+#else
             if (g + 2 < total) issue(g + 2);
+#endif
             mfma_step(acc, fa[(kKS - 1) & 1], fb[(kKS - 1) & 1]);
         }
         // ---- epilogue of tile t (see above)
