@@ -16,13 +16,17 @@
 // wave moves 8 one-KiB pieces per stage (waves 0-3 the corpus tile, 4-7 the query tile) with
 // global_load_lds_dwordx4 in the saddr form: one per-piece 32-bit lane offset fixed for the
 // whole launch, one scalar base per stage, one M0 write per four pieces (instruction offsets).
-// Per stage: k-steps 0..2 (fragments of step c+1 read while step c's 8 MFMAs run), wait for the
-// own DMA of the next stage, barrier, read the next stage's first fragments and issue the DMA of
-// the stage after it into the slot just read, k-step 3.  After a tile's last stage the top-k
-// epilogue runs without barriers (it touches no stage memory).
-// Measured (profiles/r01_ablation_*): MFMA + fragment reads alone 2.74 ms of 3.8 at 1M x 1024 x
-// 1968; the LDS-DMA traffic (64 KiB per stage against 2048 MFMA cycles per SIMD) adds ~0.65 ms
-// even when never waited for, the epilogue ~0.4 ms.
+// Per stage: k-steps 0..2 (fragments of step c+1 read under step c's 8 MFMAs, two reads per MFMA
+// gap), wait for the own DMA of the next stage, barrier, read the next stage's first fragments;
+// the corpus-tile waves (0-3) then issue the DMA of the stage after it into the slot just read
+// while the query-tile waves (4-7, static priority 1) run k-step 3's MFMAs, and the query-tile
+// waves issue theirs one k-step later, so each SIMD's MFMA pipe has a feeder during either
+// wave's DMA issue.  After a tile's last stage the top-k epilogue runs without barriers (it
+// touches no stage memory).
+// Measured with per-tile s_memtime stamps (-DIMGREC_B16_STAMPS, tools/b16_stamps.py; profiles/
+// r02/b16_stamps.txt) at 1M x 1024 x 1968: a 31-stage tile = ~76k cycles of stage loop (~2450 per
+// stage against 2048 of MFMA: the barrier and the corpus-tile waves' DMA issue) + ~14k of
+// epilogue (screen ~3.5k, ~12 insertion rounds).
 
 // LDS image: row r of a stage, 16-B chunk c stored at chunk c ^ ((r >> 1) & 7) (two 128-B rows
 // per 256-B bank row); the XOR is applied on the DMA's per-lane global source offset, so every
@@ -129,22 +133,24 @@ __device__ __forceinline__ void barrier_lds() {
 }
 
 // Ascending register list; labels arrive in increasing order per lane, so an equal key lands
-// behind the entries already present (ties by smaller label).
+// behind the entries already present (ties by smaller label).  c[p]: d goes before slot p (on the
+// old list; monotone in p); slot p takes slot p-1's entry when d goes before p-1, else d when it
+// goes before p — on an ascending list that key select is the median of (kd[p-1], d, kd[p]), one
+// v_med3.  No control flow: the selects are marked unpredictable so they stay v_cndmask instead
+// of exec-mask branches (the branchy form cost ~10 % of the epilogue), and d = +inf is a no-op.
 template <int K>
 __device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float d, int id) {
-    // c[p]: d goes before slot p (on the old list; monotone in p).  Slot p takes slot p-1's entry
-    // when d goes before p-1, else d when it goes before p: one compare, four selects per slot.
     bool c[K];
 #pragma unroll
     for (int p = 0; p < K; ++p) c[p] = d < kd[p];
 #pragma unroll
     for (int p = K - 1; p > 0; --p) {
-        // the same select on an ascending list is the median of (kd[p-1], d, kd[p]): one v_med3
         kd[p] = __builtin_amdgcn_fmed3f(kd[p - 1], d, kd[p]);
-        ki[p] = c[p - 1] ? ki[p - 1] : (c[p] ? id : ki[p]);
+        const int nx = __builtin_unpredictable(c[p]) ? id : ki[p];
+        ki[p] = __builtin_unpredictable(c[p - 1]) ? ki[p - 1] : nx;
     }
-    kd[0] = c[0] ? d : kd[0];
-    ki[0] = c[0] ? id : ki[0];
+    kd[0] = __builtin_unpredictable(c[0]) ? d : kd[0];
+    ki[0] = __builtin_unpredictable(c[0]) ? id : ki[0];
 }
 
 // (d1, i1) ranks before (d2, i2): smaller key, ties by smaller label (empty = label -1 last).
@@ -168,6 +174,15 @@ __device__ __forceinline__ void insert_any(float (&kd)[K], int (&ki)[K], float d
 }
 
 }  // namespace
+
+#ifdef IMGREC_B16_STAMPS
+// diagnostic build only (tools/b16_stamps.py): s_memtime per wave at fixed points of one tile
+__device__ unsigned long long g_b16_stamps[8 * 256];
+#define B16_STAMP(slot) do { if (stamp_on && lane == 0) { \
+    unsigned long long v_ = __builtin_amdgcn_s_memtime(); g_b16_stamps[wave * 256 + (slot)] = v_; } } while (0)
+#else
+#define B16_STAMP(slot) do {} while (0)
+#endif
 
 template <int KM, int L2>
 __global__ void __launch_bounds__(512, 2)
@@ -330,18 +345,20 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 #pragma unroll
         for (int h = 0; h < 2; ++h) fb[h] = *reinterpret_cast<const u32x4*>(sb + aoff[c] + boff + h * 32 * kRowB);
     };
+    // MFMAs i0 .. i1-1 of a k-step (i = 4 h + rb)
+    auto mfma_part = [&](f32x16 (&acc)[4][2], const u32x4 (&fa)[4], const u32x4 (&fb)[2], int i0, int i1) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = i0; i < i1; ++i)
+            acc[i & 3][i >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                __builtin_bit_cast(bf16x8, fa[i & 3]), __builtin_bit_cast(bf16x8, fb[i >> 2]), acc[i & 3][i >> 2], 0, 0, 0);
+    };
     auto mfma_step = [&](f32x16 (&acc)[4][2], const u32x4 (&fa)[4], const u32x4 (&fb)[2]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-                acc[rb][h] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                    __builtin_bit_cast(bf16x8, fa[rb]), __builtin_bit_cast(bf16x8, fb[h]), acc[rb][h], 0, 0, 0);
+        mfma_part(acc, fa, fb, 0, 8);
     };
 
     u32x4 fa[2][4], fb[2][2];
     int g = 0;
-    int pend = -1;
+    int pend = -1;                                              // deferred DMA stage
     // ---- main loop.  One barrier per stage, placed before the stage's last k-step: by then every
     // wave has read the whole stage (its slot is refilled with stage g + 2 right after) and waited
     // for its own DMA of stage g + 1, so the next stage's first fragments are read after the
@@ -354,6 +371,9 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
         read_frags(smem, 0, fa[0], fb[0]);
     }
     for (int t = t0; t < t1; ++t) {
+#ifdef IMGREC_B16_STAMPS
+        const bool stamp_on = blockIdx.x == 100 && t - t0 < 120;
+#endif
         f32x16 acc[4][2];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
@@ -363,16 +383,26 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             const char* sb = smem + (g & 1) * kStage;
 #pragma unroll
             for (int c = 0; c + 1 < kKS; ++c) {
+                // the 8 MFMAs with the next k-step's 6 fragment reads placed two per MFMA gap after
+                // each of the first three (a third read in one gap saturates the LDS array)
                 read_frags(sb, c + 1, fa[(c + 1) & 1], fb[(c + 1) & 1]);
                 mfma_step(acc, fa[c & 1], fb[c & 1]);
-#ifndef IMGREC_B16_NO_STAGGER
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // DS read
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                // the query-tile waves issue their DMA here, one k-step after the corpus-tile
+                // waves issued theirs, so each SIMD's other wave keeps the MFMA pipe busy
                 if (c == 0 && pend >= 0) {
                     __builtin_amdgcn_sched_barrier(0);
                     issue(pend);
                     pend = -1;
                     __builtin_amdgcn_sched_barrier(0);
                 }
-#endif
             }
             // (the fences keep the compiler from sinking k-step kKS-2's MFMAs below the wait)
             __builtin_amdgcn_sched_barrier(0);
@@ -382,17 +412,17 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             __builtin_amdgcn_sched_barrier(0);
             // (after a tile's last stage the next fragments are read after the epilogue instead)
             if (s + 1 < nst) read_frags(smem + ((g + 1) & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
-#ifndef IMGREC_B16_NO_STAGGER
             if (g + 2 < total) {
                 if (isA) issue(g + 2);
                 else pend = g + 2;
             }
-#else
-            if (g + 2 < total) issue(g + 2);
-#endif
             mfma_step(acc, fa[(kKS - 1) & 1], fb[(kKS - 1) & 1]);
         }
         // ---- epilogue of tile t (see above)
+        B16_STAMP(2 * (t - t0));
+#ifdef IMGREC_B16_STAMPS
+        int nit = 0;
+#endif
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
@@ -467,15 +497,20 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
                     park[64 + lane] = make_float4(acc[rb][h][8 * hf + 4], acc[rb][h][8 * hf + 5],
                                                   acc[rb][h][8 * hf + 6], acc[rb][h][8 * hf + 7]);
                     while (__any(mh != 0)) {
-                        if (mh) {
-                            const int r8 = __builtin_ctz(mh);
-                            mh &= mh - 1u;
-                            const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
-                            const int r = 8 * hf + r8;
-                            const int tr = rbase + (r & 3) + 8 * (r >> 2);
-                            const float kv = key_of(a, tr);
-                            if (kv < kd[h][KM - 1]) insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
-                        }
+#ifdef IMGREC_B16_STAMPS
+                        ++nit;
+#endif
+                        // straight-line round: a lane with nothing left inserts +inf (a no-op on
+                        // an ascending list), so the round has no divergent branches
+                        const bool act = mh != 0u;
+                        const int r8 = act ? __builtin_ctz(mh) : 0;
+                        mh &= mh - 1u;
+                        const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
+                        const int r = 8 * hf + r8;
+                        const int tr = rbase + (r & 3) + 8 * (r >> 2);
+                        float kv = key_of(a, tr);
+                        kv = __builtin_unpredictable(act && kv < kd[h][KM - 1]) ? kv : INFINITY;
+                        insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
                     }
                 }
             }
@@ -487,6 +522,10 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
             const float jb = fmaxf(kd[h][kJ - 1], __shfl_xor(kd[h][kJ - 1], 32, 64));
             if (lh == 0) share[((wr * 4 + wq) * 2 + h) * 32 + li] = jb;
         }
+        B16_STAMP(2 * (t - t0) + 1);
+#ifdef IMGREC_B16_STAMPS
+        if (stamp_on && lane == 0) g_b16_stamps[wave * 256 + 128 + (t - t0)] = (unsigned long long)nit;
+#endif
         if (g < total) read_frags(smem + (g & 1) * kStage, 0, fa[kKS & 1], fb[kKS & 1]);
     }
 
@@ -560,3 +599,9 @@ hipError_t launch_b16_big(const TileArgs& a, hipStream_t st) {
 
 }  // namespace imgrec
 
+
+#ifdef IMGREC_B16_STAMPS
+extern "C" int knn_b16_stamps_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(imgrec::g_b16_stamps), sizeof(imgrec::g_b16_stamps));
+}
+#endif
