@@ -37,6 +37,6 @@ def test_pmc_records_are_the_newest_matching(tmp_path, monkeypatch):
 def test_committed_records_cover_the_bench_kernel():
     _, pat = bench.kernel_pattern(256, 256, 2, 10)
     bytes_, src = bench.pmc_traffic(pat)
-    assert src == "r01_v16_traffic.json" and 5e9 < bytes_ < 7e9     # 1.5x the 3.97 GB bf16 corpus
+    assert src.endswith("_traffic.json") and 5e9 < bytes_ < 7e9     # 1.5x the 3.97 GB bf16 corpus
     rec, src = bench.pmc_record(pat, "_clock.json")
-    assert src == "r01_v16_clock.json" and 0.0 < rec["mfma_busy"] < 1.0
+    assert src.endswith("_clock.json") and 0.0 < rec["mfma_busy"] < 1.0
