@@ -182,12 +182,16 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
     }
 
 
-def kernel_pattern(tile_rows: int, tile_queries: int, path: int, k: int):
-    """(display name, regex) of the fused kernel a search ran: knn_b16_tile_kernel<KM, L2> for the
-    256 x 256-tile bf16 kernel, else knn_tile_topk_kernel<WR, WQ, KM, NS, BK, MODE, WB> (MODE 0
+def kernel_pattern(tile_rows: int, tile_queries: int, path: int, k: int, name: str = ""):
+    """(display name, regex) of the fused kernel a search ran: `name` from knn_plan_kernel for the
+    256 x 256-tile bf16 kernels (knn_b16w_tile_kernel<KM, L2, PACK>, or the 32 x 32-MFMA form
+    knn_b16_tile_kernel<KM, L2>), else knn_tile_topk_kernel<WR, WQ, KM, NS, BK, MODE, WB> (MODE 0
     fp32, 1 split, 2 bf16)."""
+    import re
     if path == 2 and tile_rows == 256 and tile_queries == 256:
-        return f"knn_b16_tile_kernel<{8 if k <= 8 else 10}, 1>", r"knn_b16_tile_kernel<\d+, 1>"
+        if not name:
+            name = f"knn_b16w_tile_kernel<{8 if k <= 8 else 10}, 1, true>"
+        return name, re.escape(name)
     wr, wq = tile_rows // 128, tile_queries // 32
     return (f"knn_tile_topk_kernel<{wr}, {wq}, ..., mode {path}>",
             rf"knn_tile_topk_kernel<{wr}, {wq}, \d+, \d+, \d+, {path}, \d+>")
@@ -348,7 +352,9 @@ def main():
         n_local = shard.local_rows
         flops = 2.0 * n_local * D_total * a.nq
         split = split_q > 0
-        kname, kpat = kernel_pattern(tr.value, tq.value, path, a.k)
+        kbuf = C.create_string_buffer(128)
+        lib.knn_plan_kernel(shard.index.handle, a.nq, a.k, kbuf, 128)
+        kname, kpat = kernel_pattern(tr.value, tq.value, path, a.k, kbuf.value.decode())
         # the committed PMC records were collected on the default workload (config 3, 1M rows,
         # 1024 queries, k = 10, one GPU); any other run reports them as null
         default_run = (world == 1 and a.config == 3 and cfg["rows"] == 1_000_000 and a.nq == 1024

@@ -57,6 +57,7 @@ SIGNATURES = {
     "knn_set_timing": (_i, [_vp, _i]),
     "knn_kernel_time": (_i, [_vp, _pd, _pi]),
     "knn_plan": (_i, [_vp, _i64, _i, _pi, _pi, _pi, _pi]),
+    "knn_plan_kernel": (_i, [_vp, _i64, _i, C.c_char_p, _i]),
     "knn_set_search_mode": (_i, [_vp, _i]),
     "knn_search_stats": (_i, [_vp, _pi64, _pi64, _pf]),
     "knn_search_stats2": (_i, [_vp, _pi64, _pi64, _pi64, _pf]),

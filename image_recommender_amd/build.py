@@ -29,7 +29,7 @@ LIB = LIBDIR / os.environ.get("IMGREC_LIB_NAME", "libimgrec.so")
 EXTRA_FLAGS = os.environ.get("IMGREC_EXTRA_FLAGS", "").split()
 ARCH = os.environ.get("IMGREC_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_refine.hip", "knn_capi.cpp", "knn_plan.cpp",
+SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_b16w.hip", "knn_refine.hip", "knn_capi.cpp", "knn_plan.cpp",
            "knn_search.cpp", "knn_multi.cpp", "knn_io.cpp", "ivfpq_capi.cpp", "color_hist.hip",
            "ingest.cpp", "ivfpq.hip"]
 HEADERS = ["knn_kernels.h", "knn_index.h", "knn_multi.h", "wave_ops.h", "../../include/imgrec_ivfpq.h",

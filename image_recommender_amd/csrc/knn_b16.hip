@@ -575,6 +575,7 @@ knn_b16_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ x
 }
 
 hipError_t launch_b16_big(const TileArgs& a, hipStream_t st) {
+    if (IMGREC_B16_MFMA16) return launch_b16_wide(a, st);
     if (a.wr != 2 || a.wq != 4 || a.dp % kBKW != 0 || a.nsplit < 1) return hipErrorInvalidValue;
     // the lane offsets are 32-bit: a tile's last group sits (kGPT - 1) * nsplit groups past its first
     if (((int64_t)(kGPT - 1) * a.nsplit * kRPP + kBQ) * a.dp * 4 + 8192 >= ((int64_t)1 << 32))

@@ -458,4 +458,27 @@ int knn_plan(const knn_index_t* cix, int64_t nq, int k, int* tr, int* tq, int* s
     return KNN_OK;
 }
 
+int knn_plan_kernel(const knn_index_t* cix, int64_t nq, int k, char* name, int cap) {
+    if (!cix || !name || cap < 1) KNN_FAIL(KNN_EINVAL, "NULL argument");
+    const knn_index* ix = cix->multi ? multi_shard(cix, 0) : cix;
+    const int64_t cn = std::min(nq, kQueryChunk);
+    const int l2 = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    if (use_b16(ix, cn, k)) {
+        const Plan p = make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb);
+        if (p.big && IMGREC_B16_MFMA16)
+            std::snprintf(name, cap, "knn_b16w_tile_kernel<%d, %d, %s>", p.km, l2, p.ib > 0 ? "true" : "false");
+        else if (p.big)
+            std::snprintf(name, cap, "knn_b16_tile_kernel<%d, %d>", p.km, l2);
+        else
+            std::snprintf(name, cap, "knn_tile_topk_kernel<%d, %d, ..., %d, ...>", p.wr, p.wq, kModeBF16);
+    } else if (use_split(ix, cn, k)) {
+        const Plan p = make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus);
+        std::snprintf(name, cap, "knn_tile_topk_kernel<%d, %d, ..., %d, ...>", p.wr, p.wq, kModeSplit);
+    } else {
+        const Plan p = make_plan(ix->ntotal, cn, k, ix->cus);
+        std::snprintf(name, cap, "knn_tile_topk_kernel<%d, %d, ..., %d, ...>", p.wr, p.wq, kModeF32);
+    }
+    return KNN_OK;
+}
+
 }  // extern "C"

@@ -66,6 +66,7 @@ struct Plan {
     int wr, wq, km, bm, bq;
     int nqb, nq_pad, ntiles, nsplit, ncand, wgs;
     bool big;                    // bf16 path: the 256 x 256-tile kernel (knn_b16.hip)
+    int ib;                      // > 0: its packed-list form with ib split-local index bits
 };
 constexpr int64_t kQueryChunk = 8192;
 Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus);

@@ -30,6 +30,7 @@ struct TileArgs {
     float* cand_d;              // nq x ncand keys
     int64_t* cand_i;            // nq x ncand labels
     int ncand;
+    int ib = 0;                 // 256 x 256 bf16 kernel: > 0 = packed lists with ib index bits
     // device-planned launch (the exact re-run of uncertified queries): when set, the kernel reads
     // {nq, nqb, nsplit, ncand} from dyn[0..3] and the grid has `grid` workgroups, those beyond
     // nqb * nsplit exiting at once
@@ -52,6 +53,8 @@ struct RerankArgs {
     int kc;
     int64_t nq;
     int k, metric;              // metric 1 = L2, otherwise inner product
+    float c_trunc = 0.f;        // candidate keys truncated toward -inf by at most c_trunc |key|
+                                // (the packed-list candidate kernel); 0 = exact approximate keys
     float c_split, c_fp;        // relative error-bound coefficients (see knn_capi.cpp); for
                                 // kModeBF16 c_split is the MFMA accumulation coefficient
     const float* q_resid;       // kModeBF16: |q - bf16(q)| per query
@@ -115,12 +118,22 @@ constexpr int kB16NS = IMGREC_B16_NS, kB16WGPCU = IMGREC_B16_WGPCU, kB16Pad = 64
 #ifndef IMGREC_B16_BIG_MINQ
 #define IMGREC_B16_BIG_MINQ 512
 #endif
+#ifndef IMGREC_B16_MFMA16
+#define IMGREC_B16_MFMA16 1
+#endif
+// packed candidate lists (knn_b16w.hip) while a split's row index fits this many bits: the
+// approximate keys keep 23 - ib mantissa bits (relative truncation <= 2^(ib - 23))
+#ifndef IMGREC_B16_PACK_MAXIB
+#define IMGREC_B16_PACK_MAXIB 14
+#endif
+constexpr int kB16PackMaxIB = IMGREC_B16_PACK_MAXIB;
 constexpr int kB16BigRows = 256, kB16BigQueries = 256, kB16BigMinQ = IMGREC_B16_BIG_MINQ;
 
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);
 hipError_t launch_tile_topk(const TileArgs& a, hipStream_t st);
 hipError_t launch_b16_big(const TileArgs& a, hipStream_t st);     // knn_b16.hip
+hipError_t launch_b16_wide(const TileArgs& a, hipStream_t st);    // knn_b16w.hip (16x16x32 form)
 hipError_t launch_merge(const float* cd, const int64_t* ci, int64_t nq, int nlists, int kin,
                         int64_t stride_q, int64_t stride_l, int k, int metric, int negate_in,
                         float* D, int64_t* I, hipStream_t st);

@@ -107,6 +107,16 @@ Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus, int dpb) {
         p.nsplit = std::max(1, std::min((cus + p.nqb - 1) / p.nqb, p.ntiles));
         p.ncand = p.nsplit * p.km;               // lists folded to one per (query, split)
         p.wgs = p.nqb * p.nsplit;
+        // packed lists (16x16 kernel): split-local row index t * 256 + tile row of every tile of
+        // the largest split must fit ib bits
+        p.ib = 0;
+        if (IMGREC_B16_MFMA16) {
+            const int64_t groups = (ntotal + 7) / 8, cnt = (groups + p.nsplit - 1) / p.nsplit;
+            const int64_t idx_max = (cnt + 31) / 32 * 256 - 1;
+            int ib = 1;
+            while ((int64_t{1} << ib) <= idx_max) ++ib;
+            if (ib <= kB16PackMaxIB) p.ib = ib;
+        }
         return p;
     }
     p.km = b16_km(k);

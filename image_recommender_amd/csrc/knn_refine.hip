@@ -196,7 +196,7 @@ constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
 
 // Error bounds of one query's certificate (DESIGN.md "bf16 path" / "Split path").
 struct QueryBounds {
-    float qn, xm, nn, e_ip, c_fp;
+    float qn, xm, nn, e_ip, c_fp, c_trunc;
     int metric;
     static constexpr float u = 1.0f / 8388608.f;   // 2^-23
     __device__ __forceinline__ QueryBounds(const RerankArgs& a, int64_t q) {
@@ -204,6 +204,7 @@ struct QueryBounds {
         qn = a.qnorm[q];
         xm = *a.xn_max;
         c_fp = a.c_fp;
+        c_trunc = a.c_trunc;
         nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
         // |approximate q.x - q.x| for every row:
         //   split: c_split |q| max|x|
@@ -227,9 +228,12 @@ struct QueryBounds {
     }
     // candidates with approximate key above this cannot reach the top k (the k best by
     // approximate key have exact keys <= a_k + E_a)
+    // (a candidate key may sit up to c_trunc |a| below the approximate key it stands for: a
+    // lower bound everywhere it bounds rows from below; added where it bounds from above)
     __device__ __forceinline__ float prefix_limit(float a_k) const {
-        return a_k + 2.02f * (bound_a(a_k) + bound_f(a_k));
+        return a_k + 2.02f * (bound_a(a_k) + bound_f(a_k) + trunc(a_k));
     }
+    __device__ __forceinline__ float trunc(float a) const { return c_trunc * fabsf(a); }
 };
 
 // Exact fp32 dot products of one query with kRerankRows rows, one wave, lane-strided float4
@@ -373,7 +377,7 @@ rerank_certify_kernel(const RerankArgs a) {
     // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
     // whenever the bounds hold; reported by knn_search_stats so tests and the bench watch it)
     if (inP) {
-        const float r = fabsf(ak - key) / (B.bound_a(ak) + B.bound_f(key));
+        const float r = fabsf(ak - key) / (B.bound_a(ak) + B.bound_f(key) + B.trunc(ak));
         atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
     }
 
@@ -483,7 +487,7 @@ second_chance_kernel(const RerankArgs a) {
                     o_lab[rank] = lb;
                     if (rank == k - 1) s_sk = kv;
                 }
-                const float r = fabsf(w_apx[s] - kv) / (B.bound_a(w_apx[s]) + B.bound_f(kv));
+                const float r = fabsf(w_apx[s] - kv) / (B.bound_a(w_apx[s]) + B.bound_f(kv) + B.trunc(w_apx[s]));
                 atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
             }
             __syncthreads();

@@ -11,6 +11,7 @@
 // Queries no certificate settles are re-run exactly by a device-planned launch of the fused fp32
 // kernel (run_fallback): the count never travels to the host, so knn_search_device enqueues a
 // whole search without waiting for the GPU.
+#include <cmath>
 #include <cstring>
 
 #include "knn_index.h"
@@ -168,6 +169,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     a.dp = ix->dpb / 2; a.qp = reinterpret_cast<const float*>(ix->qb16); a.qnorm = qnorm;
     a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
     a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand;
+    a.ib = p.big ? p.ib : 0;
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
     KNN_HIP(p.big ? launch_b16_big(a, st) : launch_tile_topk(a, st));
@@ -187,6 +189,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = b16_acc_coef(ix->dpb);
     r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+    r.c_trunc = a.ib > 0 ? (float)std::ldexp(1.0, a.ib - 23) : 0.f;
     r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
     r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = km;
     r.raw_stride_q = p.ncand;

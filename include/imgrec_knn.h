@@ -185,6 +185,10 @@ int knn_last_path(const knn_index_t* index);
 int knn_plan(const knn_index_t* index, int64_t nq, int k, int* tile_rows, int* tile_queries,
              int* splits, int* workgroups);
 
+/* Name of the fused candidate/distance kernel a search of nq queries launches, as profilers print
+ * it (e.g. "knn_b16w_tile_kernel<10, 1, true>"), NUL-terminated into name[cap]. */
+int knn_plan_kernel(const knn_index_t* index, int64_t nq, int k, char* name, int cap);
+
 const char* knn_last_error(void);
 const char* knn_version(void);
 

@@ -10,18 +10,22 @@ import bench
 
 
 def test_kernel_pattern_names_the_bf16_tile_kernel():
-    name, pat = bench.kernel_pattern(256, 256, 2, 10)
-    assert name == "knn_b16_tile_kernel<10, 1>"
+    name, pat = bench.kernel_pattern(256, 256, 2, 10)            # default: the 16x16 packed form
+    assert name == "knn_b16w_tile_kernel<10, 1, true>"
+    assert re.search(pat, "void imgrec::knn_b16w_tile_kernel<10, 1, true>")
+    assert not re.search(pat, "void imgrec::knn_b16_tile_kernel<10, 1>")
+    name, pat = bench.kernel_pattern(256, 256, 2, 10, "knn_b16_tile_kernel<10, 1>")   # 32x32 form
     assert re.search(pat, "void imgrec::knn_b16_tile_kernel<10, 1>")
+    assert not re.search(pat, "void imgrec::knn_b16w_tile_kernel<10, 1, true>")
     name, pat = bench.kernel_pattern(256, 32, 2, 10)             # small-batch generic kernel
     assert re.search(pat, "void imgrec::knn_tile_topk_kernel<2, 1, 16, 2, 32, 2, 4>")
-    assert not re.search(pat, "void imgrec::knn_b16_tile_kernel<10, 1>")
+    assert not re.search(pat, "void imgrec::knn_b16w_tile_kernel<10, 1, true>")
 
 
 def test_pmc_records_are_the_newest_matching(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
-    kern = "void imgrec::knn_b16_tile_kernel<10, 1>"
+    kern = "void imgrec::knn_b16w_tile_kernel<10, 1, true>"
     for v, b in ((7, 1.0), (16, 2.0), (9, 3.0)):
         (prof / f"r01_v{v}_traffic.json").write_text(json.dumps({kern: {"hbm_bytes_per_launch": b}}))
     (prof / "r01_v20_traffic.json").write_text(json.dumps({"other_kernel": {"hbm_bytes_per_launch": 9.0}}))

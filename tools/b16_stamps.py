@@ -30,7 +30,7 @@ for _ in range(4):
 torch.cuda.synchronize()
 lib = _lib.load()
 buf = (C.c_ulonglong * (8 * 256))()
-assert lib.knn_b16_stamps_read(buf) == 0
+assert getattr(lib, os.environ.get("IMGREC_STAMPS_FN", "knn_b16_stamps_read"))(buf) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(8, 256).astype(np.int64)
 nst = -(-D // 64)
 ntile = int((a[0, :128] != 0).sum() // 2)
