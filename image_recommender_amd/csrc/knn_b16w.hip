@@ -29,6 +29,8 @@
 #include <stdint.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "knn_kernels.h"
 
 namespace imgrec {
@@ -66,11 +68,6 @@ constexpr int kQuads = 8;                 // MFMA quads per stage (2 k-steps x 4
 #define IMGREC_B16W_DEFER_Q 3
 #endif
 constexpr int kDeferQ = IMGREC_B16W_DEFER_Q;
-// >= 0: the corpus-tile waves issue half their pieces after the barrier, the rest after this quad
-#ifndef IMGREC_B16W_ASPLIT_Q
-#define IMGREC_B16W_ASPLIT_Q -1
-#endif
-constexpr int kASplitQ = IMGREC_B16W_ASPLIT_Q;
 static_assert(kBKW == 32 && kCPR == 8, "stage depth: two 32-deep k-steps per stage");
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
@@ -307,19 +304,16 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
     int c_it = t0, c_is = 0;
     const uint32_t* c_tile = isA ? xh + (size_t)trow(t0, 0) * dw : qblk;
     int c_ng = (isA && t0 == t1 - 1) ? cnt - t0 * kGPT : kGPT;
-    // part 0: all of the wave's pieces of stage g; 1 / 2: the first / second half of them (the
-    // corpus-tile waves may spread their issue over two points of a stage, IMGREC_B16W_ASPLIT_Q).
-    // The cursor advances with part 0 or 2.
-    auto issue = [&](int g, int part) __attribute__((always_inline)) {
+    auto issue = [&](int g) __attribute__((always_inline)) {
         const uint32_t* src = c_tile + c_is * kBKW;
         const uint32_t dst = smem0 + (uint32_t)((g & (kNS - 1)) * kStage) + pdst;
         if (pbase + kLPW <= c_ng || !isA) {
 #pragma unroll
             for (int h = 0; h < kLPW / 4; ++h)
-                if (part == 0 || (part == 1) == (h < kLPW / 8))
-                    dma4x(src, dst + 4096u * h, voff_of(4 * h), voff_of(4 * h + 1), voff_of(4 * h + 2),
-                          voff_of(4 * h + 3));
-        } else if (part != 2) {
+                dma4x(src, dst + 4096u * h, voff_of(4 * h), voff_of(4 * h + 1), voff_of(4 * h + 2),
+                      voff_of(4 * h + 3));
+        } else {
+            // the split's last, partial tile: pieces past its groups are skipped
 #pragma unroll
             for (int j = 0; j < kLPW; ++j)
                 if (pbase + j < c_ng) {
@@ -332,10 +326,10 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                     }
                 }
         }
-        if (part != 2 && c_is == 0 && wave < 4)
+        if (c_is == 0 && wave < 4)
             dma4_norm(xnorm + trow(c_it, wave * 64 + lane),
                       smem0 + (uint32_t)(kNormOff + ((c_it - t0) & (kNormSlots - 1)) * kBM * 4 + wave * 256));
-        if (part != 1 && ++c_is == nst) {
+        if (++c_is == nst) {
             c_is = 0;
             ++c_it;
             if (isA) {
@@ -372,12 +366,12 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
 
     u32x4 fa[2][4], fb[2][2];
     int g = 0;
-    int pend = -1, pend_a = -1;
+    int pend = -1;
     if (total > 0) {
-        issue(0, 0);
+        issue(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();
-        if (total > 1) issue(1, 0);
+        if (total > 1) issue(1);
         read_a(smem, 0, fa[0]);
         read_b(smem, 0, fb[0]);
     }
@@ -391,65 +385,66 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
         for (int rb = 0; rb < kRB; ++rb)
 #pragma unroll
             for (int h = 0; h < 2; ++h) acc[rb][h] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < nst; ++s, ++g) {
-            const char* sb = smem + (g & 1) * kStage;
+        // live quad rows (64 tile rows each) of this tile: a split's partial last tile runs the
+        // MFMAs, fragment reads and screens of its live row blocks only
+        const int nlive = (t + 1) * kGPT <= cnt ? 4 : (((cnt - t * kGPT) * kRPP + 63) >> 6);
+        // one tile's stages with NR live quad rows: per stage 2 k-steps x NR quads, quad i =
+        // (k-step i / NR, quad row i % NR); the next quad's fragments are read under the current
+        // one's MFMAs (the second k-step's B fragments under the first k-step's last quad); the
+        // barrier sits before the last quad, after which the next stage's first fragments are
+        // read and the corpus-tile waves issue the DMA of the stage after it
+        auto stage_loop = [&](auto nr_tag) __attribute__((always_inline)) {
+            constexpr int NR = decltype(nr_tag)::value, L = 2 * NR;
+            for (int s = 0; s < nst; ++s, ++g) {
+                const char* sb = smem + (g & 1) * kStage;
 #pragma unroll
-            for (int q = 0; q + 1 < kQuads; ++q) {
-                // next quad's 4 A fragments (+ the second k-step's B fragments under quad 3),
-                // one read per MFMA gap
-                read_a(sb, q + 1, fa[(q + 1) & 1]);
-                if (q == 3) read_b(sb, 1, fb[1]);
-                mfma_quad(acc, fa[q & 1], fb[q >> 2], q);
+                for (int i = 0; i + 1 < L; ++i) {
+                    read_a(sb, 4 * ((i + 1) / NR) + (i + 1) % NR, fa[(i + 1) & 1]);
+                    if (i == NR - 1) read_b(sb, 1, fb[1]);
+                    mfma_quad(acc, fa[i & 1], fb[i / NR], 4 * (i / NR) + i % NR);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-                }
-                if (q == 3) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                } else {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                    for (int j = 0; j < 4; ++j) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                    }
+                    if (i == NR - 1) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                    } else {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (i == (kDeferQ < L - 2 ? kDeferQ : L - 2) && pend >= 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        issue(pend);
+                        pend = -1;
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (q == kDeferQ && pend >= 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    issue(pend, 0);
-                    pend = -1;
-                    __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                barrier_lds();
+                __builtin_amdgcn_sched_barrier(0);
+                if (s + 1 < nst) {
+                    const char* nb = smem + ((g + 1) & 1) * kStage;
+                    read_a(nb, 0, fa[0]);
+                    read_b(nb, 0, fb[0]);
                 }
-                if (kASplitQ >= 0 && q == kASplitQ && pend_a >= 0) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    issue(pend_a, 2);
-                    pend_a = -1;
-                    __builtin_amdgcn_sched_barrier(0);
+                if (g + 2 < total) {
+                    if (isA) issue(g + 2);
+                    else pend = g + 2;
                 }
+                mfma_quad(acc, fa[1], fb[1], 4 + NR - 1);
             }
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            barrier_lds();
-            __builtin_amdgcn_sched_barrier(0);
-            if (s + 1 < nst) {
-                const char* nb = smem + ((g + 1) & 1) * kStage;
-                read_a(nb, 0, fa[0]);
-                read_b(nb, 0, fb[0]);
-            }
-            if (g + 2 < total) {
-                if (!isA) {
-                    pend = g + 2;
-                } else if (kASplitQ >= 0) {
-                    issue(g + 2, 1);
-                    pend_a = g + 2;
-                } else {
-                    issue(g + 2, 0);
-                }
-            }
-            mfma_quad(acc, fa[1], fb[1], kQuads - 1);
-        }
+        };
+        if (nlive >= 4) stage_loop(std::integral_constant<int, 4>{});
+        else if (nlive == 3) stage_loop(std::integral_constant<int, 3>{});
+        else if (nlive == 2) stage_loop(std::integral_constant<int, 2>{});
+        else stage_loop(std::integral_constant<int, 1>{});
 
         // ---- top-k epilogue of tile t.  Screen: a row matters only if its key beats T = min(the
         // K-th of any of the query's four lane lists, max over them of their J-th best) — four
@@ -474,6 +469,7 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
         };
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
+            if (rg >= nlive) break;
             // row group rg = row blocks 4 rg .. 4 rg + 3; bit 4 j + i of a mask = accumulator
             // register i of row block 4 rg + j = tile row (4 rg + j) * 16 + 4 lq + i
             screen();
