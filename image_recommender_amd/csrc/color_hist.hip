@@ -121,8 +121,8 @@ __device__ __forceinline__ void count_granule(uint32_t* __restrict__ col, const 
 }
 
 template <int BINS, int P0>
-__device__ __forceinline__ void count_body(uint32_t* __restrict__ col, const uint4* __restrict__ vb,
-                                           int64_t ngran, int tid) {
+__device__ __forceinline__ void count_body_lds(uint32_t* __restrict__ col, const uint4* __restrict__ vb,
+                                               int64_t ngran, int tid) {
     // software pipeline: the loads of granule g + NT are in flight while granule g is counted
     int64_t g = tid;
     if (g >= ngran) return;
@@ -134,6 +134,174 @@ __device__ __forceinline__ void count_body(uint32_t* __restrict__ col, const uin
         a = an; b = bn; c = cn;
     }
     count_granule<BINS, P0>(col, a, b, c);
+}
+
+// Register (SWAR) counting for 16 bins, bin = top nibble of the byte (color_hist16_kernel).
+// Loads are fully coalesced: in iteration m thread tid reads the 16-B vectors
+// c = NT (3m + j) + tid, j = 0..2.  As 16 = NT = 1 (mod 3), byte i of vector j has channel
+// (lp + j + i) mod 3 with the lane's fixed phase lp = (phase of the first vector + tid) mod 3, so
+// the counters are kept per SLOT k = (j + i) mod 3 (compile-time) and mapped to channel
+// (lp + k) mod 3 only when flushed.  Per slot one u64 of sixteen 4-bit counters: a byte adds
+// 1 << (4 * bin) (the shift amounts of a word's four bytes come from one shift-and-mask,
+// (w >> 2) & 0x3c3c3c3c; a 64-bit shift uses the low 6 bits of its amount) — a 64-bit shift and
+// a 64-bit add per byte, no LDS atomic.  After vectors 1 and 2 of an iteration (<= 11 counts per
+// slot since the last widening) the nibbles are widened into two u64 of eight 8-bit counters per
+// slot (even / odd bins), which are flushed into 48 u32 register totals every 11 iterations
+// (<= 242 per 8-bit counter).  No per-thread LDS columns: 16 waves per CU and two iterations of
+// loads in flight per thread keep enough bytes in flight for HBM (the LDS-column form held 12
+// waves with one iteration in flight and ran at ~4.5 TB/s whether its counting was LDS atomics
+// or registers).
+struct Swar16 {
+    uint64_t r4[3] = {0, 0, 0};
+    uint64_t a8[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+    uint32_t tot[3][16] = {};                            // per SLOT
+    __device__ __forceinline__ void widen() {
+        constexpr uint64_t M = 0x0f0f0f0f0f0f0f0full;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            a8[k][0] += r4[k] & M;
+            a8[k][1] += (r4[k] >> 4) & M;
+            r4[k] = 0;
+        }
+    }
+    __device__ __forceinline__ void flush() {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int f = 0; f < 8; ++f) {
+                tot[k][2 * f] += (uint32_t)(a8[k][0] >> (8 * f)) & 0xffu;
+                tot[k][2 * f + 1] += (uint32_t)(a8[k][1] >> (8 * f)) & 0xffu;
+            }
+            a8[k][0] = a8[k][1] = 0;
+        }
+    }
+    // one 16-B vector whose byte i goes to slot (K0 + i) mod 3
+    template <int K0>
+    __device__ __forceinline__ void vec(const uint4& v) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t t = (w[q] >> 2) & 0x3c3c3c3cu;             // 4 * bin of each byte
+            asm volatile("" : "+v"(t));   // keep the word-wide mask (else it is re-split per byte)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r4[(K0 + 4 * q + j) % 3] += (uint64_t)1 << ((t >> (8 * j)) & 63u);
+        }
+    }
+};
+
+// 16-bin counting of nvec 16-B vectors vb[0 .. nvec) (first byte at channel phase0) into S.tot
+__device__ __forceinline__ void count_swar16(Swar16& S, const uint4* __restrict__ vb, int64_t nvec, int tid) {
+    const int64_t nit = nvec / (3 * NT);                 // full iterations (3 vectors per thread)
+    int since = 0;
+    if (nit > 0) {
+        // two iterations of loads in flight: three register sets in a fixed ring, the loop
+        // unrolled by three so no set is copied (a rotating copy made the compiler wait for
+        // every outstanding load at the top of each iteration); loads past the last iteration
+        // re-read it
+        auto ld = [&](int64_t m, uint4 (&v)[3]) __attribute__((always_inline)) {
+            const int64_t b = (m < nit ? m : nit - 1) * 3 * NT + tid;
+            v[0] = vb[b]; v[1] = vb[b + NT]; v[2] = vb[b + 2 * NT];
+        };
+        auto run = [&](const uint4 (&v)[3]) __attribute__((always_inline)) {
+            S.vec<0>(v[0]);
+            S.vec<1>(v[1]);
+            S.widen();
+            S.vec<2>(v[2]);
+            S.widen();
+            if (++since == 11) { S.flush(); since = 0; }
+        };
+        uint4 A[3], B[3], C[3];
+        ld(0, A);
+        ld(1, B);
+        for (int64_t m = 0; m < nit; m += 3) {
+            ld(m + 2, C);
+            run(A);
+            if (m + 1 >= nit) break;
+            ld(m + 3, A);
+            run(B);
+            if (m + 2 >= nit) break;
+            ld(m + 4, B);
+            run(C);
+        }
+    }
+    // remaining < 3 NT vectors: vector c = 3 NT nit + r NT + tid, phase (lp + r) mod 3
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int64_t cidx = 3 * NT * nit + (int64_t)r * NT + tid;
+        if (cidx < nvec) {
+            const uint4 v = vb[cidx];
+            if (r == 0) S.vec<0>(v); else if (r == 1) S.vec<1>(v); else S.vec<2>(v);
+        }
+        S.widen();
+    }
+    S.flush();
+}
+
+__global__ void __launch_bounds__(NT)
+color_hist16_kernel(const uint8_t* __restrict__ pix, const int64_t* __restrict__ offsets,
+                    const int64_t* __restrict__ npix, float* __restrict__ out,
+                    uint32_t* __restrict__ counts) {
+    constexpr int nb = 48;
+    __shared__ uint32_t part[NT / 64][nb];               // per-wave totals
+    __shared__ uint32_t edge[nb];                        // head / tail bytes
+    __shared__ float tot[nb];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < nb) edge[tid] = 0u;
+    __syncthreads();
+    const int64_t img = blockIdx.x;
+    const int64_t nbytes = 3 * npix[img];
+    const uint8_t* base = pix + offsets[img];
+    auto count1 = [&](int64_t o) {
+        atomicAdd(&edge[(int)(o % 3) * 16 + (base[o] >> 4)], 1u);
+    };
+    const int64_t head = std::min<int64_t>(nbytes, (int64_t)((16 - ((uintptr_t)base & 15)) & 15));
+    if (tid < head) count1(tid);
+    const int64_t nvec = (nbytes - head) >> 4;
+    Swar16 S;
+    count_swar16(S, reinterpret_cast<const uint4*>(base + head), nvec, tid);
+    for (int64_t o = head + 16 * nvec + tid; o < nbytes; o += NT) count1(o);   // < 16 bytes
+    // slot k of this lane = channel (lp + k) mod 3: rotate to channel order, then sum the wave
+    const int lp = (int)((head % 3 + tid) % 3);
+    uint32_t byc[3][16];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            const uint32_t k0 = S.tot[(3 + ch - 0) % 3][b], k1 = S.tot[(3 + ch - 1) % 3][b], k2 = S.tot[(3 + ch - 2) % 3][b];
+            byc[ch][b] = lp == 0 ? k0 : (lp == 1 ? k1 : k2);     // slot (ch - lp) mod 3
+        }
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch)
+#pragma unroll
+        for (int b = 0; b < 16; ++b) {
+            uint32_t v = byc[ch][b];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) part[wave][ch * 16 + b] = v;
+        }
+    __syncthreads();
+    if (tid < nb) {
+        uint32_t v = edge[tid];
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) v += part[w][tid];
+        tot[tid] = (float)v;
+        if (counts) counts[img * nb + tid] = v;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        float ss = 0.f;
+        for (int b = lane; b < nb; b += 64) ss = fmaf(tot[b], tot[b], ss);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+        const float l2 = sqrtf(ss);
+        for (int b = lane; b < nb; b += 64) out[img * nb + b] = (l2 != 0.f) ? tot[b] / l2 : tot[b];
+    }
+}
+
+template <int BINS, int P0>
+__device__ __forceinline__ void count_body(uint32_t* __restrict__ col, const uint4* __restrict__ vb,
+                                           int64_t ngran, int tid) {
+    count_body_lds<BINS, P0>(col, vb, ngran, tid);
 }
 
 template <int BINS>
@@ -245,8 +413,13 @@ int color_hist_device(const uint8_t* pixels, const int64_t* offsets, const int64
         return -1;
     }
     if (bins == 16) {
+#ifdef IMGREC_COLOR_LDS_ATOMIC
         hipLaunchKernelGGL(color_hist_fixed_kernel<16>, dim3((unsigned)n_images), dim3(NT), 0,
                            (hipStream_t)stream, pixels, offsets, npix, out, counts);
+#else
+        hipLaunchKernelGGL(color_hist16_kernel, dim3((unsigned)n_images), dim3(NT), 0,
+                           (hipStream_t)stream, pixels, offsets, npix, out, counts);
+#endif
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("color_hist_fixed_kernel launch failed: %s", hipGetErrorString(e));

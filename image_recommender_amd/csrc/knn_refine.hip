@@ -342,21 +342,47 @@ rerank_certify_kernel(const RerankArgs a) {
         const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
         return reinterpret_cast<const float4*>(a.xb + (l - id_offset) * dp);
     };
-    for (int c0 = wave; c0 < m; c0 += kRerankWaves * kRerankRows) {
-        const float4* r4[kRerankRows];
-        float acc[kRerankRows];
+    // candidates [c_begin, c_end), kRerankWaves * kRerankRows rows in flight per round
+    auto rerank_range = [&](int c_begin, int c_end) {
+        for (int c0 = c_begin + wave; c0 < c_end; c0 += kRerankWaves * kRerankRows) {
+            const float4* r4[kRerankRows];
+            float acc[kRerankRows];
 #pragma unroll
-        for (int v = 0; v < kRerankRows; ++v)
-            r4[v] = row_of(min(c0 + kRerankWaves * v, m - 1));   // clamped: loads unconditional
-        rerank_dots<IT>(q4, qr, n4, lane, r4, acc);
+            for (int v = 0; v < kRerankRows; ++v)
+                r4[v] = row_of(min(c0 + kRerankWaves * v, c_end - 1));   // clamped: loads unconditional
+            rerank_dots<IT>(q4, qr, n4, lane, r4, acc);
 #pragma unroll
-        for (int v = 0; v < kRerankRows; ++v) {
-            const int c = c0 + kRerankWaves * v;
-            if (lane == c && c < m) skey[c] = rerank_key(acc[v], B.qn, a.xn[lab - id_offset], metric);
+            for (int v = 0; v < kRerankRows; ++v) {
+                const int c = c0 + kRerankWaves * v;
+                if (lane == c && c < c_end) skey[c] = rerank_key(acc[v], B.qn, a.xn[lab - id_offset], metric);
+            }
         }
-    }
+    };
     if (wave == 0) slab[lane] = lab;
+    // Two phases: the first P1 candidates, then — with s1 = the k-th exact key among them (an
+    // upper bound of the final k-th) — only the candidates c with a_c - E_a(a_c) <= s1 + E_f(s1)
+    // (any other has exact key > s1 + E_f(s1): v - E_a(v) is increasing, and a truncated key is
+    // below the approximate key it stands for).  The refined prefix replaces a_k's twice-bounded
+    // limit; its first candidate left out passes the certificate by construction.
+    constexpr int P1 = kRerankWaves * kRerankRows;
+    const int m1 = min(m, P1);
+    rerank_range(0, m1);
     __syncthreads();
+    if (m > m1) {
+        if (m1 >= k) {                                  // (k > P1: the whole prefix, one phase)
+            const float key1 = lane < m1 ? skey[lane] : INFINITY;
+            int r1 = 0;
+            for (int i = 0; i < m1; ++i)
+                if (lane < m1 && ranks_before_r(skey[i], slab[i], key1, lab)) ++r1;
+            const uint64_t hit = __ballot(lane < m1 && r1 == k - 1);
+            const float s1 = __shfl(key1, hit ? (int)__builtin_ctzll(hit) : 0, 64);
+            const float lim = s1 + B.bound_f(s1);
+            const int m2 = __popcll(__ballot(valid && lane < m && ak - B.bound_a(ak) <= lim));
+            m = max(m1, m2);
+        }
+        rerank_range(m1, m);
+        __syncthreads();
+    }
     if (wave != 0) return;
     const float key = lane < m ? skey[lane] : INFINITY;
 
