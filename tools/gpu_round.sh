@@ -5,7 +5,7 @@ export PYTHONPATH=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 TAG=${1:-run}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 2; }
 cat $OUT/bench.json
