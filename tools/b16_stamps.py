@@ -17,6 +17,8 @@ from image_recommender_amd.faiss_compat import METRIC_L2
 from image_recommender_amd.sharded import ShardedIndex
 
 cfg = dict(bench.CONFIGS[3])
+if os.environ.get("IMGREC_STAMPS_ROWS"):       # e.g. 125000: the N = 8 shard
+    cfg["rows"] = int(os.environ["IMGREC_STAMPS_ROWS"])
 dev = torch.device("cuda", 0)
 D = int(sum(cfg["parts"]))
 centres = bench.make_centres(torch, cfg, dev, 3)
