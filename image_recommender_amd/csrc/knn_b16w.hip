@@ -519,17 +519,17 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                         mh &= mh - 1u;
                         const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
                         const int tr = (rb0 + (r8 >> 2)) * 16 + 4 * lq + (r8 & 3);
-                        float kv;
-                        if (L2) {
-                            kv = fmaf(-2.f, a, qn[h] + nrm[tr]);
-                            kv = kv < 0.f ? 0.f : kv;
-                        } else {
-                            kv = -a;
-                        }
+                        float kv = L2 ? fmaf(-2.f, a, qn[h] + nrm[tr]) : -a;
                         if constexpr (PACK) {
-                            const uint32_t u = (ord_bits(kv) & ~lowm) | (uint32_t)(t * kBM + tr);
+                            // L2: the clamp at 0 and the order map in two integer ops — a key
+                            // with the sign bit set (negative or -0) maps to ord(+0) = 2^31, a
+                            // non-negative one to its bits | 2^31
+                            const uint32_t ob = L2 ? ((uint32_t)max((int)__float_as_uint(kv), 0) | 0x80000000u)
+                                                   : ord_bits(kv);
+                            const uint32_t u = (ob & ~lowm) | (uint32_t)(t * kBM + tr);
                             insert_packed<KM>(kp[h], __builtin_unpredictable(act) ? u : ~0u);
                         } else {
+                            if (L2) kv = kv < 0.f ? 0.f : kv;
                             kv = __builtin_unpredictable(act && kv < kd[h][KM - 1]) ? kv : INFINITY;
                             insert_mono<KM>(kd[h], ki[h], kv, trow(t, tr));
                         }
