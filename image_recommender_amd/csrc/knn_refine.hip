@@ -402,9 +402,11 @@ rerank_certify_kernel(const RerankArgs a) {
 
     // observed |approx - rerank| of every reranked candidate relative to the two bounds (<= 1
     // whenever the bounds hold; reported by knn_search_stats so tests and the bench watch it)
-    if (inP) {
-        const float r = fabsf(ak - key) / (B.bound_a(ak) + B.bound_f(key) + B.trunc(ak));
-        atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+    {   // one same-address atomic per query, not one per reranked candidate
+        float r = inP ? fabsf(ak - key) / (B.bound_a(ak) + B.bound_f(key) + B.trunc(ak)) : 0.f;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) r = fmaxf(r, __shfl_xor(r, off, 64));
+        if (lane == 0 && m > 0) atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
     }
 
     // certificate: tau = smallest approximate key a row outside the prefix can have — the K'-th

@@ -1,7 +1,7 @@
 """ShardedIndex.search end to end on the GPU: two ranks (gloo, both on cuda:0 — the 8-GPU RCCL run
 belongs to the driver) each hold a row shard, search into their packed chunk, gather it in one
 collective and merge with knn_merge_packed_device; the result equals one index over all rows
-(SURVEY.md §8e)."""
+(SURVEY.md §8e), and both agree with the float64 oracle (tests/knn_check.py contract)."""
 import os
 import socket
 
@@ -70,6 +70,8 @@ def test_sharded_search_two_ranks_equals_one_index(faiss, n, d, nq, k, mode):
     full.add(xb)
     full.search_mode = mode
     Df, If = full.search(xq, k)
+    from tests.knn_check import check_knn
+    check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)      # the sharded result vs the oracle
     if fallbacks or full.search_stats()[1]:
         assert (I == If).mean() > 0.99
         return
