@@ -12,6 +12,8 @@ sharding sees the same rows.
 A step = one batch of Q queries searched against the whole corpus: on N GPUs each rank searches its
 contiguous row shard (fused distance + top-k kernel), the per-shard (Q, k) results are all-gathered
 over RCCL and merged (strong scaling: the corpus is fixed, per-GPU rows shrink as N grows).
+`--query-groups 2` runs the query x row partition instead (sharded.py; measured slower per rank at
+N = 2/4/8: profiles/r02/qr_shapes.jsonl).
 
 Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1) prints ONE JSON line
 on rank 0.  `value` = Q*K / max-over-ranks wall time of the K steps, inputs resident in HBM.
@@ -57,6 +59,8 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="override corpus rows (total)")
     ap.add_argument("--nq", type=int, default=1024, help="queries per batch")
     ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--query-groups", type=int, default=1,
+                    help="query slices of the N ranks (sharded.py query x row partition)")
     ap.add_argument("--gt-queries", type=int, default=128, help="queries checked for recall@k")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -108,8 +112,9 @@ def gen_queries(torch, cfg, centres, nq, device, seed):
 
 
 # ------------------------------------------------------------------------------------------------
-def exact_ground_truth(torch, dist, world, cfg, centres, r0, r1, q, k, device, seed):
-    """float64 exact top-k of this rank's shard, gathered and merged (recall reference)."""
+def exact_ground_truth(torch, dist, world, cfg, centres, r0, r1, q, k, device, seed, rshards=None):
+    """float64 exact top-k of this rank's shard, gathered and merged (recall reference); with a
+    query x row partition the first `rshards` ranks hold every row once."""
     qd = q.double()
     qn = (qd * qd).sum(1, keepdim=True)
     best_d = torch.full((q.shape[0], k), float("inf"), dtype=torch.float64, device=device)
@@ -130,7 +135,8 @@ def exact_ground_truth(torch, dist, world, cfg, centres, r0, r1, q, k, device, s
         gi = [torch.empty_like(best_i) for _ in range(world)]
         dist.all_gather(gd, best_d)
         dist.all_gather(gi, best_i)
-        cat_d, cat_i = torch.cat(gd, 1), torch.cat(gi, 1)
+        keep = rshards or world
+        cat_d, cat_i = torch.cat(gd[:keep], 1), torch.cat(gi[:keep], 1)
         v2, j = torch.topk(cat_d, k, dim=1, largest=False)
         best_d, best_i = v2, torch.gather(cat_i, 1, j)
     return best_d.cpu().numpy(), best_i.cpu().numpy()
@@ -249,10 +255,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world > 1:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    # IMGREC_DIST_BACKEND=gloo rehearses the N-rank protocol with every rank on one visible GPU
+    # (local % device count); the measured runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("IMGREC_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     from image_recommender_amd import _lib
     from image_recommender_amd.faiss_compat import METRIC_L2
@@ -266,7 +280,9 @@ def main():
     centres = make_centres(torch, cfg, device, seed)
     q = gen_queries(torch, cfg, centres, a.nq, device, seed)
 
-    shard = ShardedIndex(D_total, cfg["rows"], METRIC_L2, device=local)
+    qgroups = a.query_groups
+    nq_local = a.nq // qgroups if a.nq % qgroups == 0 else a.nq      # queries one rank searches
+    shard = ShardedIndex(D_total, cfg["rows"], METRIC_L2, device=local, query_groups=qgroups)
     t_build0 = time.perf_counter()
     for blk in gen_rows(torch, cfg, centres, shard.row0, shard.row1, device, seed):
         shard.add_local(blk)
@@ -313,7 +329,7 @@ def main():
     # recall@k on the first gt-queries queries, against float64 exact ground truth
     ngt = min(a.gt_queries, a.nq)
     gt_d, gt_i = exact_ground_truth(torch, dist, world, cfg, centres, shard.row0, shard.row1,
-                                    q[:ngt], a.k, device, seed)
+                                    q[:ngt], a.k, device, seed, shard.rshards)
     got_i = Ir[:ngt].cpu().numpy()
     got_d = Dr[:ngt].cpu().numpy()
     hits = sum(len(set(x.tolist()) & set(y.tolist())) for x, y in zip(got_i, gt_i))
@@ -342,7 +358,7 @@ def main():
     path1 = lib.knn_last_path(shard.index.handle)          # 0 exact, 1 split, 2 bf16
 
     tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
-    lib.knn_plan(shard.index.handle, a.nq, a.k, C.byref(tr), C.byref(tq), C.byref(sp), C.byref(wg))
+    lib.knn_plan(shard.index.handle, nq_local, a.k, C.byref(tr), C.byref(tq), C.byref(sp), C.byref(wg))
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -350,10 +366,10 @@ def main():
 
     if rank == 0:
         n_local = shard.local_rows
-        flops = 2.0 * n_local * D_total * a.nq
+        flops = 2.0 * n_local * D_total * nq_local
         split = split_q > 0
         kbuf = C.create_string_buffer(128)
-        lib.knn_plan_kernel(shard.index.handle, a.nq, a.k, kbuf, 128)
+        lib.knn_plan_kernel(shard.index.handle, nq_local, a.k, kbuf, 128)
         kname, kpat = kernel_pattern(tr.value, tq.value, path, a.k, kbuf.value.decode())
         # the committed PMC records were collected on the default workload (config 3, 1M rows,
         # 1024 queries, k = 10, one GPU); any other run reports them as null
@@ -397,7 +413,9 @@ def main():
             "config": {
                 "workload": cfg["name"], "rows": cfg["rows"], "dim": D_total, "k": a.k,
                 "queries_per_batch": a.nq, "metric": cfg["ranking"],
-                "rows_per_gpu": n_local, "parallelism": f"row-shard x{world} + RCCL all-gather merge",
+                "rows_per_gpu": n_local, "parallelism": (f"query-slice x{qgroups} * row-shard x{world // qgroups}" if qgroups > 1
+                                else f"row-shard x{world}") + " + RCCL all-gather merge",
+                "queries_per_gpu": nq_local,
                 "tile_rows": tr.value, "tile_queries": tq.value, "row_splits": sp.value,
                 "workgroups": wg.value,
             },
@@ -415,7 +433,7 @@ def main():
                 "mfma_busy": busy[0]["mfma_busy"] if busy else None,
                 "clock_ghz": busy[0]["clock_ghz"] if busy else None,
                 "busy_source": busy[1] if busy else None,
-                "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{a.nq} flop per launch",
+                "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{nq_local} flop per launch",
             },
             "single_query": {
                 "queries_per_s": a.single_query_steps / el1,

@@ -9,6 +9,14 @@ latency-bound, far below one xGMI link) and merges the
 G*k candidates per query with the same (key, label) order as a single-GPU search, so sharded and
 unsharded results are identical.
 
+Query x row partition (``query_groups`` Q > 1): the world is Q groups of R = world / Q ranks;
+rank r holds row shard r % R of R (rows replicated Q times — a 1M x 1968 corpus is 12 GB per
+copy, HBM has 288 GB) and searches query slice r // R of Q against it.  The candidate kernel does
+the same MFMA work per rank as the pure row partition (its row splits keep the same length), while
+every per-query cost after it — candidate merge, rerank + certificate, the packed chunk — falls by
+Q.  One all-gather still moves every chunk; each rank then merges, per query slice, that slice's R
+row-shard chunks.  Results are identical to the row partition's (and to one index).
+
 The reference has no multi-device code at all; this module replaces nothing but extends
 ``index.search`` (main/search_from_image.py:247) to corpora larger than one GPU.
 """
@@ -25,6 +33,21 @@ from .faiss_compat import METRIC_L2, Index, _METRIC_TO_KNN
 def shard_range(ntotal: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous balanced row range of `rank` (same formula as the kernel's row splits)."""
     return ntotal * rank // world, ntotal * (rank + 1) // world
+
+
+def partition(world: int, rank: int, query_groups: int = 1) -> tuple[int, int, int]:
+    """(query slice, row shard, row shards) of `rank` in a query_groups x (world / query_groups)
+    partition (query_groups = 1: the pure row partition)."""
+    if query_groups < 1 or world % query_groups:
+        raise ValueError(f"query_groups={query_groups} must divide the world size {world}")
+    rshards = world // query_groups
+    return rank // rshards, rank % rshards, rshards
+
+
+def query_slices(nq: int, query_groups: int) -> int:
+    """Queries per slice, or 0 when the batch does not split evenly: then every group searches
+    the whole batch and the merge reads group 0's chunks (the same answer, redundant work)."""
+    return nq // query_groups if query_groups > 1 and nq % query_groups == 0 else 0
 
 
 def gather_results(D, I, group=None):
@@ -92,12 +115,17 @@ def gather_packed(buf, group=None, out=None):
     return g
 
 
-def merge_packed_device(g, nq: int, kin: int, k: int, metric: int = METRIC_L2, stream: int = 0):
-    """HIP merge (knn_merge_packed_device) of gathered packed chunks (world, nbytes) -> (nq, k)."""
+def merge_packed_device(g, nq: int, kin: int, k: int, metric: int = METRIC_L2, stream: int = 0,
+                        out=None):
+    """HIP merge (knn_merge_packed_device) of gathered packed chunks (nchunks, nbytes) -> (nq, k)
+    (out: optional contiguous (D, I) views to write into)."""
     import torch
     world = g.shape[0]
-    D = torch.empty((nq, k), dtype=torch.float32, device=g.device)
-    I = torch.empty((nq, k), dtype=torch.int64, device=g.device)
+    if out is not None:
+        D, I = out
+    else:
+        D = torch.empty((nq, k), dtype=torch.float32, device=g.device)
+        I = torch.empty((nq, k), dtype=torch.int64, device=g.device)
     _lib.check(_lib.load().knn_merge_packed_device(
         C.c_void_p(g.data_ptr()), int(world), int(nq), int(kin), int(k), _METRIC_TO_KNN[metric],
         C.c_void_p(D.data_ptr()), C.c_void_p(I.data_ptr()), C.c_void_p(stream or None)),
@@ -109,14 +137,16 @@ class ShardedIndex:
     """This rank's shard of a row-partitioned exact index, plus the collective search."""
 
     def __init__(self, d: int, ntotal_global: int, metric: int = METRIC_L2, group=None,
-                 device: int | None = None):
+                 device: int | None = None, query_groups: int = 1):
         import torch
         import torch.distributed as dist
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.d, self.metric, self.ntotal_global = int(d), metric, int(ntotal_global)
-        self.row0, self.row1 = shard_range(self.ntotal_global, self.rank, self.world)
+        self.query_groups = int(query_groups)
+        self.qslice, self.rshard, self.rshards = partition(self.world, self.rank, self.query_groups)
+        self.row0, self.row1 = shard_range(self.ntotal_global, self.rshard, self.rshards)
         dev = torch.cuda.current_device() if device is None else device
         self.device = dev
         self.index = Index(d, metric, dev)
@@ -148,14 +178,26 @@ class ShardedIndex:
             I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
             self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
             return D, I
-        # the shard searches straight into its packed chunk; one all-gather moves keys and labels
-        # (chunk and gather buffers are kept per (nq, k): every call is stream-ordered on them)
+        # the shard searches its query slice straight into its packed chunk; one all-gather moves
+        # keys and labels (chunk and gather buffers are kept per (nq, k): every call is
+        # stream-ordered on them)
+        per = query_slices(nq, self.query_groups)
+        nql = per or nq
+        ql = q[self.qslice * per:(self.qslice + 1) * per] if per else q
         key = (nq, k, q.device)
         if key not in self._packed:
-            buf = torch.empty(packed_layout(nq, k)[0], dtype=torch.uint8, device=q.device)
+            buf = torch.empty(packed_layout(nql, k)[0], dtype=torch.uint8, device=q.device)
             g = torch.empty((self.world, buf.numel()), dtype=torch.uint8, device=q.device)
-            self._packed = {key: (buf, g) + packed_views(buf, nq, k)}
+            self._packed = {key: (buf, g) + packed_views(buf, nql, k)}
         buf, g, D, I = self._packed[key]
-        self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
+        ql = ql.contiguous()
+        self.index.search_device(ql.data_ptr(), nql, k, D.data_ptr(), I.data_ptr(), st)
         gather_packed(buf, self.group, out=g)
-        return merge_packed_device(g, nq, k, k, self.metric, st)
+        if not per:      # every slice searched the whole batch: group 0's row-shard chunks
+            return merge_packed_device(g[:self.rshards], nq, k, k, self.metric, st)
+        Do = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+        Io = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+        for s in range(self.query_groups):   # slice s: chunks s*R .. s*R + R - 1
+            merge_packed_device(g[s * self.rshards:(s + 1) * self.rshards], per, k, k, self.metric,
+                                st, out=(Do[s * per:(s + 1) * per], Io[s * per:(s + 1) * per]))
+        return Do, Io

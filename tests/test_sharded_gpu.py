@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, d, nq, k, mode, out):
+def _worker(rank, world, port, n, d, nq, k, mode, out, qgroups=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
@@ -37,7 +37,7 @@ def _worker(rank, world, port, n, d, nq, k, mode, out):
         torch.cuda.set_device(0)
         xb = mixture(n, d, centres=40, seed=31)
         xq = torch.from_numpy(mixture(nq, d, centres=40, seed=32)).cuda()
-        sh = ShardedIndex(d, n, METRIC_L2, device=0)
+        sh = ShardedIndex(d, n, METRIC_L2, device=0, query_groups=qgroups)
         sh.add_local(xb[sh.row0:sh.row1])
         sh.index.search_mode = mode
         for _ in range(2):                                  # second call: cached chunk buffers
@@ -50,15 +50,19 @@ def _worker(rank, world, port, n, d, nq, k, mode, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,d,nq,k,mode", [(20000, 96, 64, 10, "exact"), (30000, 256, 600, 10, "bf16"),
-                                           (4001, 64, 7, 5, "exact")])
-def test_sharded_search_two_ranks_equals_one_index(faiss, n, d, nq, k, mode):
+@pytest.mark.parametrize("n,d,nq,k,mode,world,qgroups", [
+    (20000, 96, 64, 10, "exact", 2, 1), (30000, 256, 600, 10, "bf16", 2, 1), (4001, 64, 7, 5, "exact", 2, 1),
+    # query x row partition: 2 query slices x 2 row shards; 2 slices of the whole corpus; an
+    # uneven batch (every slice searches all 7 queries)
+    (30000, 256, 600, 10, "bf16", 4, 2), (20000, 96, 64, 10, "exact", 2, 2), (4001, 64, 7, 5, "exact", 4, 2)])
+def test_sharded_search_two_ranks_equals_one_index(faiss, n, d, nq, k, mode, world, qgroups):
     import torch.multiprocessing as mp
     from tests.datagen import mixture
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, d, nq, k, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, d, nq, k, mode, q, qgroups))
+             for r in range(world)]
     for p in procs:
         p.start()
     D, I, fallbacks = q.get(timeout=240)
