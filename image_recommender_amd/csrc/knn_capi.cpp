@@ -129,8 +129,9 @@ int create_single(int d, int metric, int device, knn_index** out) {
     DeviceGuard g(device);
     knn_index* ix = new knn_index();
     ix->d = d;
-    // rows padded to 16 floats; from d >= 512 to 32 so the 32-deep staging path applies
-    ix->dp = (int)round_up(d, d >= 512 ? 2 * kDepthPad : kDepthPad);
+    // rows padded to 16 floats; from d >= 256 to 32, so the 32-deep staging path and the split
+    // copy (32-float stages) serve every d the split path takes
+    ix->dp = (int)round_up(d, d >= 256 ? 2 * kDepthPad : kDepthPad);
     ix->metric = metric;
     ix->device = device;
     ix->split_ok = ix->dp % 32 == 0 && d >= 256;
@@ -413,7 +414,7 @@ int knn_set_search_mode(knn_index_t* ix, int mode) {
     if (ix->multi) return multi_set_search_mode(ix, mode);
     std::lock_guard<std::mutex> lk(ix->mu);
     if (mode == KNN_SEARCH_SPLIT && !ix->split_ok)
-        KNN_FAIL(KNN_EINVAL, "split search needs d >= 256 (rows padded to 32 floats); d = %d", ix->d);
+        KNN_FAIL(KNN_EINVAL, "split search needs d >= 256; d = %d", ix->d);
     if (mode == KNN_SEARCH_BF16 && !ix->b16_ok)
         KNN_FAIL(KNN_EINVAL, "bf16 search needs d >= 64; d = %d", ix->d);
     ix->mode = mode;

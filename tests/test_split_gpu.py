@@ -36,7 +36,7 @@ def _index(faiss, d, metric):
     return faiss.IndexFlat(d, faiss.METRIC_COSINE)
 
 
-@pytest.mark.parametrize("d", [256, 512, 768, 1968])
+@pytest.mark.parametrize("d", [256, 300, 392, 512, 768, 1968])     # 300, 392: rows padded to 32
 @pytest.mark.parametrize("nq", [1, 130, 300])
 def test_split_l2_shapes(faiss, d, nq):
     xb = mixture(6000, d, centres=50, seed=d)

@@ -1,0 +1,77 @@
+"""Randomised sweep of the search paths against the float64 oracle (tests/knn_check.py contract).
+
+Each case draws a corpus size, dimension (odd ones included: padding paths), batch size, k
+(up to KNN_MAX_K = 32), metric and search mode (auto / exact / split / bf16), adds the corpus in
+one or several calls (regrowth), and checks the result of index.search
+(main/search_from_image.py:247) against oracle.flat_knn.  Forcing a mode on a shape it does not
+serve (split: d < 256; bf16: d < 64) must raise at the setter, and the case then runs in auto.
+The case list is fixed by its seed, so a failure reproduces by its id.
+"""
+import numpy as np
+import pytest
+
+from tests.datagen import mixture
+from tests.knn_check import check_knn
+
+pytestmark = pytest.mark.gpu
+
+_MODES = ("auto", "exact", "split", "bf16")
+_METRICS = ("l2", "ip", "cosine")
+
+
+def _cases(n_cases=40, seed=2026):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n_cases):
+        n = int(rng.choice([1, 7, 255, 256, 257, 1000, 4099, 20000, 70000]))
+        d = int(rng.choice([3, 16, 47, 64, 130, 256, 300, 512, 768, 1968]))
+        nq = int(rng.choice([1, 2, 31, 33, 129, 257, 520, 1100]))
+        k = int(rng.choice([1, 3, 10, 16, 17, 32]))
+        metric = _METRICS[int(rng.integers(0, 3))]
+        mode = _MODES[int(rng.integers(0, 4))]
+        adds = int(rng.choice([1, 1, 3]))
+        if n * d > 40_000_000:                  # keep every case a few seconds of oracle work
+            n = 40_000_000 // d
+        out.append(pytest.param(n, d, nq, k, metric, mode, adds, 1000 + i, id=f"c{i}"))
+    return out
+
+
+@pytest.fixture(scope="module")
+def faiss(gpu):
+    from image_recommender_amd import faiss_compat
+    return faiss_compat
+
+
+@pytest.mark.parametrize("n,d,nq,k,metric,mode,adds,seed", _cases())
+def test_random_case_matches_oracle(faiss, n, d, nq, k, metric, mode, adds, seed):
+    xb = mixture(n, d, centres=max(2, min(60, n // 4)), seed=seed)
+    xq = mixture(nq, d, centres=max(2, min(60, n // 4)), seed=seed + 1)
+    if metric == "l2":
+        idx = faiss.IndexFlatL2(d)
+    elif metric == "ip":
+        idx = faiss.IndexFlatIP(d)
+    else:
+        idx = faiss.IndexFlat(d, faiss.METRIC_COSINE)
+    from image_recommender_amd._lib import KnnError
+    unsupported = (mode == "split" and d < 256) or (mode == "bf16" and d < 64)
+    if unsupported:
+        with pytest.raises(KnnError):
+            idx.search_mode = mode
+    else:
+        idx.search_mode = mode
+    for part in np.array_split(xb, adds):
+        if len(part):
+            idx.add(np.ascontiguousarray(part))
+    assert idx.ntotal == n
+    D, I = idx.search(xq, k)
+    assert D.shape == (nq, k) and I.shape == (nq, k)
+    check_knn(D, I, xb, xq, k, metric, min_exact_frac=0.0)
+
+
+def test_k_above_limit_raises(faiss):
+    """k > KNN_MAX_K is refused loudly (the fused top-k keeps register lists)."""
+    from image_recommender_amd._lib import KNN_MAX_K
+    idx = faiss.IndexFlatL2(64)
+    idx.add(mixture(100, 64, seed=1))
+    with pytest.raises(NotImplementedError):
+        idx.search(mixture(2, 64, seed=2), KNN_MAX_K + 1)
