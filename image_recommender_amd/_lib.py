@@ -16,7 +16,8 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / os.environ.get("IMGREC_LIB_
 # Error codes of include/imgrec_knn.h
 KNN_OK, KNN_EINVAL, KNN_EHIP, KNN_ENOMEM, KNN_EIO, KNN_ENOSYS = 0, -1, -2, -3, -4, -5
 KNN_METRIC_IP, KNN_METRIC_L2, KNN_METRIC_COSINE = 0, 1, 2
-KNN_MAX_K = 32
+KNN_MAX_K = 32          # fused top-k kernels (include/imgrec_knn.h)
+KNN_MAX_K_LARGE = 1024  # largest k of a search (GEMM + select beyond KNN_MAX_K)
 KNN_SEARCH_AUTO, KNN_SEARCH_EXACT, KNN_SEARCH_SPLIT, KNN_SEARCH_BF16 = 0, 1, 2, 3
 COLOR_HIST_MAX_BINS = 32
 INGEST_NOT_FAST, INGEST_TOO_SMALL = -1, -2

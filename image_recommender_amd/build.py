@@ -31,7 +31,7 @@ ARCH = os.environ.get("IMGREC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_b16w.hip", "knn_refine.hip", "knn_capi.cpp", "knn_plan.cpp",
            "knn_search.cpp", "knn_multi.cpp", "knn_io.cpp", "ivfpq_capi.cpp", "color_hist.hip",
-           "ingest.cpp", "ivfpq.hip"]
+           "ingest.cpp", "ivfpq.hip", "knn_largek.hip"]
 HEADERS = ["knn_kernels.h", "knn_index.h", "knn_multi.h", "wave_ops.h", "../../include/imgrec_ivfpq.h",
            "../../include/imgrec_knn.h", "../../include/imgrec_color.h", "../../include/imgrec_ingest.h"]
 
@@ -74,7 +74,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
     if force or _stale(LIB, objs):
         tmp = LIB.with_suffix(".so.tmp")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + \
-              [str(o) for o in objs]
+              [str(o) for o in objs] + ["-lrocblas"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -164,6 +164,7 @@ void free_single(knn_index* ix) {
                     (void*)ix->qsplit, (void*)ix->cand2_d, (void*)ix->cand2_i, (void*)ix->fail,
                     (void*)ix->fb_q, (void*)ix->fb_qn, (void*)ix->hq, (void*)ix->hd, (void*)ix->hi})
         if (p) (void)hipFree(p);
+    largek_free(ix);
     for (hipEvent_t e : ix->ev) (void)hipEventDestroy(e);
     if (ix->fence) (void)hipEventDestroy(ix->fence);
     (void)hipStreamDestroy(ix->stream);
@@ -307,7 +308,8 @@ int knn_reconstruct_n(const knn_index_t* cix, int64_t i0, int64_t n, float* x) {
 int knn_search_device(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                       void* stream) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (k <= 0 || k > KNN_MAX_K) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K, k);
+    if (k <= 0 || k > (ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE))
+        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE, k);
     if (nq < 0 || (nq > 0 && (!q || !D || !I))) KNN_FAIL(KNN_EINVAL, "bad query/output pointers");
     if (nq == 0) return KNN_OK;
     if (ix->multi) return multi_search_device(ix, q, nq, k, D, I, (hipStream_t)stream);
@@ -322,7 +324,8 @@ int knn_search_device(knn_index_t* ix, const float* q, int64_t nq, int k, float*
 
 int knn_search(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (k <= 0 || k > KNN_MAX_K) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K, k);
+    if (k <= 0 || k > (ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE))
+        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE, k);
     if (nq < 0 || (nq > 0 && (!q || !D || !I))) KNN_FAIL(KNN_EINVAL, "bad query/output pointers");
     if (nq == 0) return KNN_OK;
     if (ix->multi) return multi_search(ix, q, nq, k, D, I);

@@ -147,6 +147,10 @@ struct knn_index {
     size_t ev_used = 0;
     // one index over several devices (knn_multi.cpp); NULL for a single-device index
     struct knn_multi* multi = nullptr;
+    // k > KNN_MAX_K (knn_largek.hip): rocBLAS handle, GEMM block, running top-k lists
+    void* blas = nullptr;
+    float* lk_g = nullptr; size_t lk_g_cap = 0;
+    uint64_t* lk_run = nullptr; size_t lk_run_cap = 0;
 };
 
 namespace imgrec {
@@ -167,6 +171,10 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
 int read_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int64_t* first_fail,
                       float* ratio);
 bool use_b16(const knn_index* ix, int64_t nq, int k);
+// knn_largek.hip
+int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
+                  hipStream_t st);
+void largek_free(knn_index* ix);
 bool use_split(const knn_index* ix, int64_t nq, int k);
 
 }  // namespace imgrec

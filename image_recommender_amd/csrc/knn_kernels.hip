@@ -751,27 +751,7 @@ hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, 
 // no insertion, the lane's list is its queue.  Entries are packed into one 64-bit value
 // (order-preserving key bits | local row), so each of the kout rounds is one wave u64 minimum
 // (wave_min_u64); the winning lane (unique: a row sits in one list) pops its head.
-// Wave-wide sum (uniform) and exclusive prefix sum of an int: DPP row_shr steps give the in-row
-// inclusive prefix, lane reads of the row totals carry it across rows.
-__device__ __forceinline__ int row_inclusive_sum(int x) {
-    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
-    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
-    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
-    return x;
-}
-__device__ __forceinline__ int wave_sum_i32(int x) {
-    const int r = row_inclusive_sum(x);
-    return __builtin_amdgcn_readlane(r, 15) + __builtin_amdgcn_readlane(r, 31) +
-           __builtin_amdgcn_readlane(r, 47) + __builtin_amdgcn_readlane(r, 63);
-}
-__device__ __forceinline__ int wave_excl_scan_i32(int x) {
-    const int r = row_inclusive_sum(x);
-    const int t0 = __builtin_amdgcn_readlane(r, 15), t1 = __builtin_amdgcn_readlane(r, 31);
-    const int t2 = __builtin_amdgcn_readlane(r, 47);
-    const int row = (int)(threadIdx.x & 63) >> 4;
-    return r - x + (row > 0 ? t0 : 0) + (row > 1 ? t1 : 0) + (row > 2 ? t2 : 0);
-}
+// (wave_sum_i32 / wave_excl_scan_i32: wave_ops.h)
 
 // A query's nlists lists may be split into G groups of <= 64 (two-level merge): wave s handles
 // group s % G of query s / G; floor_in (optional, G per output row of the previous level) is

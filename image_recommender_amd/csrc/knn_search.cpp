@@ -264,6 +264,10 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     ix->last_split_queries = 0;
     ix->stat_valid = false;
+    if (k > KNN_MAX_K) {               // register top-k lists end at 32: faiss's GEMM + select form
+        ix->last_path = 0;
+        return largek_search(ix, q, nq, k, D, I, st);
+    }
     if (ix->ntotal == 0) {
         KNN_HIP(launch_fill_empty(D, I, nq * (int64_t)k, kmetric, st));
         return KNN_OK;

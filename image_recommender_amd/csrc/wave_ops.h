@@ -46,4 +46,26 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return m;
 }
 
+// Wave-wide sum (uniform) and exclusive prefix sum of an int: DPP row_shr steps give the in-row
+// inclusive prefix, lane reads of the row totals carry it across rows.
+__device__ __forceinline__ int row_inclusive_sum(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    return x;
+}
+__device__ __forceinline__ int wave_sum_i32(int x) {
+    const int r = row_inclusive_sum(x);
+    return __builtin_amdgcn_readlane(r, 15) + __builtin_amdgcn_readlane(r, 31) +
+           __builtin_amdgcn_readlane(r, 47) + __builtin_amdgcn_readlane(r, 63);
+}
+__device__ __forceinline__ int wave_excl_scan_i32(int x) {
+    const int r = row_inclusive_sum(x);
+    const int t0 = __builtin_amdgcn_readlane(r, 15), t1 = __builtin_amdgcn_readlane(r, 31);
+    const int t2 = __builtin_amdgcn_readlane(r, 47);
+    const int row = (int)(threadIdx.x & 63) >> 4;
+    return r - x + (row > 0 ? t0 : 0) + (row > 1 ? t1 : 0) + (row > 2 ? t2 : 0);
+}
+
 }  // namespace imgrec

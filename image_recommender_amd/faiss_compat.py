@@ -44,7 +44,7 @@ from types import SimpleNamespace
 import numpy as np
 
 from . import _lib
-from ._lib import KNN_MAX_K, KnnError
+from ._lib import KNN_MAX_K, KNN_MAX_K_LARGE, KnnError
 
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
@@ -157,8 +157,8 @@ class Index:
         k = int(k)
         if k <= 0:
             raise ValueError("k must be positive")
-        if k > KNN_MAX_K:
-            raise NotImplementedError(f"k={k} exceeds the fused top-k limit of {KNN_MAX_K}")
+        if k > KNN_MAX_K_LARGE:
+            raise NotImplementedError(f"k={k} exceeds the search limit of {KNN_MAX_K_LARGE}")
         n = x.shape[0]
         D = np.empty((n, k), dtype=np.float32) if D is None else D
         I = np.empty((n, k), dtype=np.int64) if I is None else I

@@ -93,8 +93,12 @@ enum knn_search_mode {
     KNN_SEARCH_BF16 = 3
 };
 
-/* Largest k one search can return (the fused top-k keeps per-lane lists of this length). */
+/* Largest k the fused top-k kernels serve (they keep per-lane lists of this length). */
 #define KNN_MAX_K 32
+/* Largest k one search can return: KNN_MAX_K < k <= KNN_MAX_K_LARGE runs faiss IndexFlat's own
+ * algorithm (fp32 GEMM blocks + an exact per-query radix select, csrc/knn_largek.hip) on a
+ * single-device index; a multi-device index (knn_create_multi) serves k <= KNN_MAX_K. */
+#define KNN_MAX_K_LARGE 1024
 
 /* Create an empty index of dimension d on HIP device `device` (-1 = current device). */
 int knn_create(int d, int metric, int device, knn_index_t** out);

@@ -1,7 +1,7 @@
 """Randomised sweep of the search paths against the float64 oracle (tests/knn_check.py contract).
 
 Each case draws a corpus size, dimension (odd ones included: padding paths), batch size, k
-(up to KNN_MAX_K = 32), metric and search mode (auto / exact / split / bf16), adds the corpus in
+(past KNN_MAX_K = 32 too: the GEMM + select path), metric and search mode (auto / exact / split / bf16), adds the corpus in
 one or several calls (regrowth), and checks the result of index.search
 (main/search_from_image.py:247) against oracle.flat_knn.  Forcing a mode on a shape it does not
 serve (split: d < 256; bf16: d < 64) must raise at the setter, and the case then runs in auto.
@@ -26,7 +26,7 @@ def _cases(n_cases=40, seed=2026):
         n = int(rng.choice([1, 7, 255, 256, 257, 1000, 4099, 20000, 70000]))
         d = int(rng.choice([3, 16, 47, 64, 130, 256, 300, 512, 768, 1968]))
         nq = int(rng.choice([1, 2, 31, 33, 129, 257, 520, 1100]))
-        k = int(rng.choice([1, 3, 10, 16, 17, 32]))
+        k = int(rng.choice([1, 3, 10, 16, 17, 32, 33, 100]))
         metric = _METRICS[int(rng.integers(0, 3))]
         mode = _MODES[int(rng.integers(0, 4))]
         adds = int(rng.choice([1, 1, 3]))
@@ -69,9 +69,26 @@ def test_random_case_matches_oracle(faiss, n, d, nq, k, metric, mode, adds, seed
 
 
 def test_k_above_limit_raises(faiss):
-    """k > KNN_MAX_K is refused loudly (the fused top-k keeps register lists)."""
-    from image_recommender_amd._lib import KNN_MAX_K
+    """k > KNN_MAX_K_LARGE is refused loudly."""
+    from image_recommender_amd._lib import KNN_MAX_K_LARGE
     idx = faiss.IndexFlatL2(64)
     idx.add(mixture(100, 64, seed=1))
     with pytest.raises(NotImplementedError):
-        idx.search(mixture(2, 64, seed=2), KNN_MAX_K + 1)
+        idx.search(mixture(2, 64, seed=2), KNN_MAX_K_LARGE + 1)
+
+
+@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
+@pytest.mark.parametrize("n,d,nq,k", [(20000, 96, 9, 33), (20000, 96, 9, 1024), (700, 64, 5, 1000),
+                                      (9000, 1968, 3, 100), (5000, 32, 2100, 40)])
+def test_large_k_matches_oracle(faiss, metric, n, d, nq, k):
+    """k > KNN_MAX_K (knn_largek.hip: fp32 GEMM blocks of 8192 - k rows, running top-k by radix
+    select): several corpus blocks, n < k (padding), 2100 queries (two query blocks)."""
+    xb = mixture(n, d, centres=40, seed=n + k)
+    xq = mixture(nq, d, centres=40, seed=n + k + 1)
+    idx = (faiss.IndexFlatL2(d) if metric == "l2" else faiss.IndexFlatIP(d) if metric == "ip"
+           else faiss.IndexFlat(d, faiss.METRIC_COSINE))
+    idx.add(xb)
+    D, I = idx.search(xq, k)
+    assert D.shape == (nq, k)
+    sel = np.arange(nq) if nq <= 16 else np.random.default_rng(0).choice(nq, 16, replace=False)
+    check_knn(D[sel], I[sel], xb, xq[sel], k, metric, min_exact_frac=0.0)
