@@ -308,8 +308,8 @@ int knn_reconstruct_n(const knn_index_t* cix, int64_t i0, int64_t n, float* x) {
 int knn_search_device(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                       void* stream) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (k <= 0 || k > (ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE))
-        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE, k);
+    if (k <= 0 || k > KNN_MAX_K_LARGE)
+        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
     if (nq < 0 || (nq > 0 && (!q || !D || !I))) KNN_FAIL(KNN_EINVAL, "bad query/output pointers");
     if (nq == 0) return KNN_OK;
     if (ix->multi) return multi_search_device(ix, q, nq, k, D, I, (hipStream_t)stream);
@@ -324,8 +324,8 @@ int knn_search_device(knn_index_t* ix, const float* q, int64_t nq, int k, float*
 
 int knn_search(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (k <= 0 || k > (ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE))
-        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", ix->multi ? KNN_MAX_K : KNN_MAX_K_LARGE, k);
+    if (k <= 0 || k > KNN_MAX_K_LARGE)
+        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
     if (nq < 0 || (nq > 0 && (!q || !D || !I))) KNN_FAIL(KNN_EINVAL, "bad query/output pointers");
     if (nq == 0) return KNN_OK;
     if (ix->multi) return multi_search(ix, q, nq, k, D, I);
@@ -351,10 +351,17 @@ int knn_search(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int
 int knn_merge_device(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin, int k,
                      int metric, float* D, int64_t* I, void* stream) {
     if (nlists <= 0 || kin <= 0 || nq < 0) KNN_FAIL(KNN_EINVAL, "bad merge shape");
-    if (k <= 0 || k > KNN_MAX_K) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K, k);
+    if (k <= 0 || k > KNN_MAX_K_LARGE) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
+    if (k > KNN_MAX_K && (int64_t)nlists * kin > 8192)
+        KNN_FAIL(KNN_EINVAL, "k > %d merges at most 8192 entries per query (%d x %d)", KNN_MAX_K, nlists, kin);
     if (nq == 0) return KNN_OK;
     if (!cD || !cI || !D || !I) KNN_FAIL(KNN_EINVAL, "NULL pointer");
     const int kmetric = metric == KNN_METRIC_L2 ? 1 : 0;
+    if (k > KNN_MAX_K) {
+        KNN_HIP(launch_merge_large(cD, cI, nlists, nq, kin, nq * (int64_t)kin, nq * (int64_t)kin, k,
+                                   kmetric, D, I, (hipStream_t)stream));
+        return KNN_OK;
+    }
     KNN_HIP(launch_merge(cD, cI, nq, nlists, kin, kin, nq * (int64_t)kin, k, kmetric,
                          kmetric ? 0 : 1, D, I, (hipStream_t)stream));
     return KNN_OK;
@@ -369,13 +376,20 @@ int64_t knn_packed_bytes(int64_t nq, int k) {
 int knn_merge_packed_device(const void* packed, int nlists, int64_t nq, int kin, int k, int metric,
                             float* D, int64_t* I, void* stream) {
     if (nlists <= 0 || kin <= 0 || nq < 0) KNN_FAIL(KNN_EINVAL, "bad merge shape");
-    if (k <= 0 || k > KNN_MAX_K) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K, k);
+    if (k <= 0 || k > KNN_MAX_K_LARGE) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
+    if (k > KNN_MAX_K && (int64_t)nlists * kin > 8192)
+        KNN_FAIL(KNN_EINVAL, "k > %d merges at most 8192 entries per query (%d x %d)", KNN_MAX_K, nlists, kin);
     if (nq == 0) return KNN_OK;
     if (!packed || !D || !I) KNN_FAIL(KNN_EINVAL, "NULL pointer");
     const int64_t n = nq * kin, nf = n + (n & 1);
     const float* cD = static_cast<const float*>(packed);
     const int64_t* cI = reinterpret_cast<const int64_t*>(static_cast<const char*>(packed) + nf * 4);
     const int kmetric = metric == KNN_METRIC_L2 ? 1 : 0;
+    if (k > KNN_MAX_K) {
+        KNN_HIP(launch_merge_large(cD, cI, nlists, nq, kin, nf + 2 * n, nf / 2 + n, k, kmetric, D, I,
+                                   (hipStream_t)stream));
+        return KNN_OK;
+    }
     // chunk = nf floats + n int64: nf + 2n floats, nf / 2 + n int64
     KNN_HIP(launch_merge_strided(cD, cI, nq, nlists, kin, kin, nf + 2 * n, nf / 2 + n, k, kmetric,
                                  kmetric ? 0 : 1, D, I, (hipStream_t)stream));

@@ -175,6 +175,10 @@ bool use_b16(const knn_index* ix, int64_t nq, int k);
 int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                   hipStream_t st);
 void largek_free(knn_index* ix);
+// merge of nlists sorted per-shard lists for KNN_MAX_K < k (nlists * kin <= 8192; labels < 2^32)
+hipError_t launch_merge_large(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin,
+                              int64_t sd, int64_t si, int k, int metric, float* D, int64_t* I,
+                              hipStream_t st);
 bool use_split(const knn_index* ix, int64_t nq, int k);
 
 }  // namespace imgrec

@@ -34,6 +34,67 @@ constexpr int kLKM = 8192;          // LDS values per query: running list + corp
 constexpr int kLKSort = 1024;       // KNN_MAX_K_LARGE, a power of two
 static_assert(KNN_MAX_K_LARGE <= kLKSort && (kLKSort & (kLKSort - 1)) == 0, "sort width");
 
+// The k smallest of v[0 .. M) (LDS, u64 values, empties = ~0) into sel[0 .. k) — ascending when
+// `sort` — by an exact radix select of the k-th smallest T (eight 8-bit digit passes of a 256-bin
+// LDS histogram), then the values < T and copies of T; the rest of sel is ~0.  Block-wide.
+__device__ void select_k(const uint64_t* v, int M, int k, uint64_t* sel, uint32_t* hist,
+                         uint64_t* s_prefix, int* s_rem, int* s_nlt, bool sort) {
+    const int t = threadIdx.x;
+    const int kk = min(k, M);
+    if (t == 0) { *s_prefix = 0; *s_rem = kk; }
+    __syncthreads();
+    uint64_t mask = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int b = t; b < 256; b += kLKThreads) hist[b] = 0u;
+        __syncthreads();
+        const uint64_t prefix = *s_prefix;
+        for (int i = t; i < M; i += kLKThreads) {
+            const uint64_t x = v[i];
+            if ((x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (t < 64) {                                   // wave 0: the digit where rem is reached
+            const uint32_t h0 = hist[4 * t], h1 = hist[4 * t + 1], h2 = hist[4 * t + 2], h3 = hist[4 * t + 3];
+            const int mine = (int)(h0 + h1 + h2 + h3);
+            const int before = wave_excl_scan_i32(mine);
+            const int rem = *s_rem;
+            if (before < rem && before + mine >= rem) {
+                int c = before, dgt = 4 * t;
+                const uint32_t hh[4] = {h0, h1, h2, h3};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (c + (int)hh[e] >= rem) { dgt = 4 * t + e; break; }
+                    c += (int)hh[e];
+                }
+                *s_prefix = prefix | ((uint64_t)dgt << shift);
+                *s_rem = rem - c;
+            }
+        }
+        mask |= (uint64_t)255 << shift;
+        __syncthreads();
+    }
+    const uint64_t T = *s_prefix;                       // the kk-th smallest value
+    if (t == 0) *s_nlt = 0;
+    __syncthreads();
+    for (int i = t; i < M; i += kLKThreads)
+        if (v[i] < T) sel[atomicAdd(s_nlt, 1)] = v[i];
+    __syncthreads();
+    const int nlt = *s_nlt;                             // < kk; the rest are copies of T
+    for (int i = nlt + t; i < kLKSort; i += kLKThreads) sel[i] = i < kk ? T : ~0ull;
+    __syncthreads();
+    if (!sort) return;
+    for (int size = 2; size <= kLKSort; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < kLKSort / 2; i += kLKThreads) {
+                const int lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint64_t a = sel[lo], b = sel[hi];
+                if ((a > b) == up) { sel[lo] = b; sel[hi] = a; }
+            }
+            __syncthreads();
+        }
+}
+
 __global__ void __launch_bounds__(kLKThreads)
 largek_select_kernel(const float* __restrict__ G, int nrc, const float* __restrict__ qnorm,
                      const float* __restrict__ xn, int64_t r0, int k, int metric, int first,
@@ -56,64 +117,11 @@ largek_select_kernel(const float* __restrict__ G, int nrc, const float* __restri
         v[nr + j] = ((uint64_t)key_bits_ordered(key) << 32) | (uint32_t)(r0 + j);
     }
     const int M = nr + nrc;
-    const int kk = min(k, M);
-    if (t == 0) { s_prefix = 0; s_rem = kk; }
-    __syncthreads();
-    // k-th smallest value, eight bits at a time from the top
-    uint64_t mask = 0;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-        for (int b = t; b < 256; b += kLKThreads) hist[b] = 0u;
-        __syncthreads();
-        const uint64_t prefix = s_prefix;
-        for (int i = t; i < M; i += kLKThreads) {
-            const uint64_t x = v[i];
-            if ((x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        if (t < 64) {                                   // wave 0: the digit where rem is reached
-            const uint32_t h0 = hist[4 * t], h1 = hist[4 * t + 1], h2 = hist[4 * t + 2], h3 = hist[4 * t + 3];
-            const int mine = (int)(h0 + h1 + h2 + h3);
-            const int before = wave_excl_scan_i32(mine);
-            const int rem = s_rem;
-            const bool here = before < rem && before + mine >= rem;
-            if (here) {
-                int c = before, dgt = 4 * t;
-                const uint32_t hh[4] = {h0, h1, h2, h3};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if (c + (int)hh[e] >= rem) { dgt = 4 * t + e; break; }
-                    c += (int)hh[e];
-                }
-                s_prefix = prefix | ((uint64_t)dgt << shift);
-                s_rem = rem - c;
-            }
-        }
-        mask |= (uint64_t)255 << shift;
-        __syncthreads();
-    }
-    const uint64_t T = s_prefix;                        // the kk-th smallest value
-    if (t == 0) s_nlt = 0;
-    __syncthreads();
-    for (int i = t; i < M; i += kLKThreads)
-        if (v[i] < T) sel[atomicAdd(&s_nlt, 1)] = v[i];
-    __syncthreads();
-    const int nlt = s_nlt;                              // < kk; the rest are copies of T
-    for (int i = nlt + t; i < kLKSort; i += kLKThreads) sel[i] = i < kk ? T : ~0ull;
-    __syncthreads();
+    select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, last != 0);
     if (!last) {
         for (int i = t; i < k; i += kLKThreads) run[q * k + i] = sel[i];
         return;
     }
-    for (int size = 2; size <= kLKSort; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = t; i < kLKSort / 2; i += kLKThreads) {
-                const int lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const uint64_t a = sel[lo], b = sel[hi];
-                if ((a > b) == up) { sel[lo] = b; sel[hi] = a; }
-            }
-            __syncthreads();
-        }
     for (int i = t; i < k; i += kLKThreads) {
         const uint64_t x = sel[i];
         if (x == ~0ull) {
@@ -127,7 +135,54 @@ largek_select_kernel(const float* __restrict__ G, int nrc, const float* __restri
     }
 }
 
+// Merge of nlists sorted per-shard results of kin entries per query (distance-ascending for L2,
+// inner-product-descending otherwise; label -1 = empty) into the final top-k for k > KNN_MAX_K:
+// list l of query q at cD[l * sd + q * kin], cI[l * si + q * kin].  Labels must be < 2^32 (they
+// pack beside the key; ties order by label, faiss's rule).
+__global__ void __launch_bounds__(kLKThreads)
+largek_merge_kernel(const float* __restrict__ cD, const int64_t* __restrict__ cI, int nlists,
+                    int kin, int64_t sd, int64_t si, int k, int metric, float* __restrict__ D,
+                    int64_t* __restrict__ I) {
+    __shared__ uint64_t v[kLKM];
+    __shared__ uint64_t sel[kLKSort];
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t s_prefix;
+    __shared__ int s_rem, s_nlt;
+    const int t = threadIdx.x;
+    const int64_t q = blockIdx.x;
+    const int M = nlists * kin;
+    for (int e = t; e < M; e += kLKThreads) {
+        const int l = e / kin, p = e - l * kin;
+        const int64_t lab = cI[l * si + q * kin + p];
+        const float d = cD[l * sd + q * kin + p];
+        v[e] = lab < 0 ? ~0ull : ((uint64_t)key_bits_ordered(metric == 1 ? d : -d) << 32) | (uint32_t)lab;
+    }
+    __syncthreads();
+    select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, true);
+    for (int i = t; i < k; i += kLKThreads) {
+        const uint64_t x = sel[i];
+        if (x == ~0ull) {
+            D[q * k + i] = metric == 1 ? FLT_MAX : -FLT_MAX;
+            I[q * k + i] = -1;
+        } else {
+            const float key = key_from_ordered((uint32_t)(x >> 32));
+            D[q * k + i] = metric == 1 ? key : -key;
+            I[q * k + i] = (int64_t)(uint32_t)x;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_merge_large(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin,
+                              int64_t sd, int64_t si, int k, int metric, float* D, int64_t* I,
+                              hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (k > KNN_MAX_K_LARGE || (int64_t)nlists * kin > kLKM) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(largek_merge_kernel, dim3((unsigned)nq), dim3(kLKThreads), 0, st, cD, cI,
+                       nlists, kin, sd, si, k, metric, D, I);
+    return hipGetLastError();
+}
 
 void largek_free(knn_index* ix) {
     if (ix->blas) (void)rocblas_destroy_handle((rocblas_handle)ix->blas);

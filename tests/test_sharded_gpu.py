@@ -54,7 +54,9 @@ def _worker(rank, world, port, n, d, nq, k, mode, out, qgroups=1):
     (20000, 96, 64, 10, "exact", 2, 1), (30000, 256, 600, 10, "bf16", 2, 1), (4001, 64, 7, 5, "exact", 2, 1),
     # query x row partition: 2 query slices x 2 row shards; 2 slices of the whole corpus; an
     # uneven batch (every slice searches all 7 queries)
-    (30000, 256, 600, 10, "bf16", 4, 2), (20000, 96, 64, 10, "exact", 2, 2), (4001, 64, 7, 5, "exact", 4, 2)])
+    (30000, 256, 600, 10, "bf16", 4, 2), (20000, 96, 64, 10, "exact", 2, 2), (4001, 64, 7, 5, "exact", 4, 2),
+    # k > KNN_MAX_K: per-shard GEMM + select, the packed large-k merge
+    (20000, 96, 33, 120, "auto", 2, 1)])
 def test_sharded_search_two_ranks_equals_one_index(faiss, n, d, nq, k, mode, world, qgroups):
     import torch.multiprocessing as mp
     from tests.datagen import mixture
@@ -77,6 +79,10 @@ def test_sharded_search_two_ranks_equals_one_index(faiss, n, d, nq, k, mode, wor
     from tests.knn_check import check_knn
     check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)      # the sharded result vs the oracle
     if fallbacks or full.search_stats()[1]:
+        assert (I == If).mean() > 0.99
+        return
+    if k > 32:      # the GEMM + select path: rounding follows the GEMM's blocking (per shard)
+        np.testing.assert_allclose(D, Df, rtol=1e-6, atol=1e-6)
         assert (I == If).mean() > 0.99
         return
     np.testing.assert_array_equal(I, If)

@@ -92,3 +92,15 @@ def test_large_k_matches_oracle(faiss, metric, n, d, nq, k):
     assert D.shape == (nq, k)
     sel = np.arange(nq) if nq <= 16 else np.random.default_rng(0).choice(nq, 16, replace=False)
     check_knn(D[sel], I[sel], xb, xq[sel], k, metric, min_exact_frac=0.0)
+
+
+@pytest.mark.parametrize("k", [50, 200])
+def test_large_k_multi_device_index(faiss, k):
+    """k > KNN_MAX_K on a multi-device index (three shards on device 0): per-shard GEMM + select,
+    then the large-k merge of the gathered lists."""
+    xb = mixture(30000, 96, centres=40, seed=k)
+    xq = mixture(7, 96, centres=40, seed=k + 1)
+    idx = faiss.IndexFlatL2(96, devices=[0, 0, 0])
+    idx.add(xb)
+    D, I = idx.search(xq, k)
+    check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.0)
