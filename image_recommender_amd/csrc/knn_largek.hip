@@ -95,11 +95,15 @@ __device__ void select_k(const uint64_t* v, int M, int k, uint64_t* sel, uint32_
         }
 }
 
+// Workgroup (query qq of the block, stripe s = blockIdx.y): the GEMM columns [s * nrc, (s + 1) *
+// nrc) of this round (ldg = the round's rows; global row r0 + s * nrc at column s * nrc) merged
+// into stripe s's running list run[(s * nq_all + q) * k ...].  With one stripe the last round
+// sorts and writes D / I; with several, largek_final_kernel merges the stripes.
 __global__ void __launch_bounds__(kLKThreads)
-largek_select_kernel(const float* __restrict__ G, int nrc, const float* __restrict__ qnorm,
+largek_select_kernel(const float* __restrict__ G, int ldg, int nrc, const float* __restrict__ qnorm,
                      const float* __restrict__ xn, int64_t r0, int k, int metric, int first,
-                     int last, int64_t q0, uint64_t* __restrict__ run, float* __restrict__ D,
-                     int64_t* __restrict__ I, int64_t id_offset) {
+                     int last, int64_t q0, int64_t nq_all, uint64_t* __restrict__ run,
+                     float* __restrict__ D, int64_t* __restrict__ I, int64_t id_offset) {
     __shared__ uint64_t v[kLKM];
     __shared__ uint64_t sel[kLKSort];
     __shared__ uint32_t hist[256];
@@ -107,21 +111,57 @@ largek_select_kernel(const float* __restrict__ G, int nrc, const float* __restri
     __shared__ int s_rem, s_nlt;
     const int t = threadIdx.x;
     const int64_t qq = blockIdx.x, q = q0 + qq;
+    const int sidx = blockIdx.y;
+    run += (int64_t)sidx * nq_all * k;
+    const int c0 = sidx * nrc;
+    const int ns = max(0, min(nrc, ldg - c0));          // this stripe's columns in the round
+    const int64_t rs = r0 + c0;
     const int nr = first ? 0 : k;
     for (int i = t; i < nr; i += kLKThreads) v[i] = run[q * k + i];
     const float qn = qnorm[q];
-    const float* g = G + qq * (int64_t)nrc;
-    for (int j = t; j < nrc; j += kLKThreads) {
+    const float* g = G + qq * (int64_t)ldg + c0;
+    for (int j = t; j < ns; j += kLKThreads) {
         // L2: (|q|^2 + |x|^2) - 2 q.x, clamped at 0; IP: -q.x (G = -2 q.x, halving is exact)
-        const float key = metric == 1 ? fmaxf((qn + xn[r0 + j]) + g[j], 0.f) : 0.5f * g[j];
-        v[nr + j] = ((uint64_t)key_bits_ordered(key) << 32) | (uint32_t)(r0 + j);
+        const float key = metric == 1 ? fmaxf((qn + xn[rs + j]) + g[j], 0.f) : 0.5f * g[j];
+        v[nr + j] = ((uint64_t)key_bits_ordered(key) << 32) | (uint32_t)(rs + j);
     }
-    const int M = nr + nrc;
+    const int M = nr + ns;
     select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, last != 0);
     if (!last) {
         for (int i = t; i < k; i += kLKThreads) run[q * k + i] = sel[i];
         return;
     }
+    for (int i = t; i < k; i += kLKThreads) {
+        const uint64_t x = sel[i];
+        if (x == ~0ull) {
+            D[q * k + i] = metric == 1 ? FLT_MAX : -FLT_MAX;
+            I[q * k + i] = -1;
+        } else {
+            const float key = key_from_ordered((uint32_t)(x >> 32));
+            D[q * k + i] = metric == 1 ? key : -key;
+            I[q * k + i] = (int64_t)(uint32_t)x + id_offset;
+        }
+    }
+}
+
+// The stripes' running lists of one query (S x k local rows) -> the final sorted top-k.
+__global__ void __launch_bounds__(kLKThreads)
+largek_final_kernel(const uint64_t* __restrict__ run, int S, int64_t nq_all, int k, int64_t q0,
+                    int metric, float* __restrict__ D, int64_t* __restrict__ I, int64_t id_offset) {
+    __shared__ uint64_t v[kLKM];
+    __shared__ uint64_t sel[kLKSort];
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t s_prefix;
+    __shared__ int s_rem, s_nlt;
+    const int t = threadIdx.x;
+    const int64_t q = q0 + blockIdx.x;
+    const int M = S * k;
+    for (int e = t; e < M; e += kLKThreads) {
+        const int sidx = e / k, i = e - sidx * k;
+        v[e] = run[((int64_t)sidx * nq_all + q) * k + i];
+    }
+    __syncthreads();
+    select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, true);
     for (int i = t; i < k; i += kLKThreads) {
         const uint64_t x = sel[i];
         if (x == ~0ull) {
@@ -216,22 +256,33 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     const rocblas_handle h = (rocblas_handle)ix->blas;
     if (rocblas_set_stream(h, st) != rocblas_status_success) KNN_FAIL(KNN_EHIP, "rocblas_set_stream failed");
     const int nrc_max = kLKM - k;
+    // Small batches: S stripes of running lists per query, so one GEMM round covers S corpus
+    // blocks (S x fewer GEMM + select launches, S workgroups per query) and a final kernel merges
+    // the S lists (S * k <= kLKM).  Large batches fill the chip with one stripe.
+    const int S = nq <= 64 ? (int)std::max<int64_t>(1, std::min<int64_t>(32, kLKM / k)) : 1;
     const int64_t nqc = std::min<int64_t>(nq, 2048);
-    if ((rc = grow(&ix->lk_g, &ix->lk_g_cap, (size_t)nqc * nrc_max)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)nq * k)) != KNN_OK) return rc;
+    const int64_t round_rows = (int64_t)S * nrc_max;
+    if ((rc = grow(&ix->lk_g, &ix->lk_g_cap, (size_t)nqc * round_rows)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)S * nq * k)) != KNN_OK) return rc;
     const float alpha = -2.f, beta = 0.f;
     for (int64_t q0 = 0; q0 < nq; q0 += nqc) {
         const int qc = (int)std::min<int64_t>(nqc, nq - q0);
-        for (int64_t r0 = 0; r0 < ix->ntotal; r0 += nrc_max) {
-            const int nrc = (int)std::min<int64_t>(nrc_max, ix->ntotal - r0);
-            // column-major: G (nrc x qc, ld nrc) = X_block^T (nrc x dp) * Q_block (dp x qc)
-            if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, nrc, qc, ix->dp,
+        for (int64_t r0 = 0; r0 < ix->ntotal; r0 += round_rows) {
+            const int m = (int)std::min<int64_t>(round_rows, ix->ntotal - r0);
+            // column-major: G (m x qc, ld m) = X_rows^T (m x dp) * Q_block (dp x qc)
+            if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, m, qc, ix->dp,
                               &alpha, ix->xb + r0 * ix->dp, ix->dp, ix->qpad + q0 * ix->dp, ix->dp,
-                              &beta, ix->lk_g, nrc) != rocblas_status_success)
+                              &beta, ix->lk_g, m) != rocblas_status_success)
                 KNN_FAIL(KNN_EHIP, "rocblas_sgemm failed");
-            hipLaunchKernelGGL(largek_select_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st,
-                               ix->lk_g, nrc, ix->qnorm, ix->xn, r0, k, kmetric, r0 == 0 ? 1 : 0,
-                               r0 + nrc >= ix->ntotal ? 1 : 0, q0, ix->lk_run, D, I, ix->id_offset);
+            const int last = (S == 1 && r0 + m >= ix->ntotal) ? 1 : 0;
+            hipLaunchKernelGGL(largek_select_kernel, dim3((unsigned)qc, (unsigned)S), dim3(kLKThreads), 0, st,
+                               ix->lk_g, m, nrc_max, ix->qnorm, ix->xn, r0, k, kmetric, r0 == 0 ? 1 : 0,
+                               last, q0, nq, ix->lk_run, D, I, ix->id_offset);
+            KNN_HIP(hipGetLastError());
+        }
+        if (S > 1) {
+            hipLaunchKernelGGL(largek_final_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st,
+                               ix->lk_run, S, nq, k, q0, kmetric, D, I, ix->id_offset);
             KNN_HIP(hipGetLastError());
         }
     }
