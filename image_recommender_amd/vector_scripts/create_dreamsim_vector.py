@@ -70,6 +70,38 @@ def _lin(m, x):
     return F.linear(x.to(w.dtype), w, m.b_lp)
 
 
+def _add_ln(x, delta, ln):
+    """x += delta (bf16, or None) in place, and the bf16 LayerNorm of the new x — one HIP pass
+    (include/imgrec_vit.h vit_add_layernorm_bf16)."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    c = x.shape[-1]
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    d = 0 if delta is None else delta.contiguous().data_ptr()
+    rc = _lib.load().vit_add_layernorm_bf16(
+        C.c_void_p(x.data_ptr()), C.c_void_p(d), C.c_void_p(ln.weight.data_ptr()),
+        C.c_void_p(ln.bias.data_ptr()), C.c_void_p(y.data_ptr()), x.numel() // c, c, float(ln.eps),
+        C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_add_layernorm_bf16 failed")
+    return y
+
+
+def _quick_gelu_(h):
+    """CLIP's QuickGELU in place on a contiguous bf16 tensor (vit_quick_gelu_bf16)."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    rc = _lib.load().vit_quick_gelu_bf16(C.c_void_p(h.data_ptr()), h.numel(),
+                                         C.c_void_p(torch.cuda.current_stream(h.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_quick_gelu_bf16 failed")
+    return h
+
+
 def build_ensemble(seed: int | None = 0, depth: int = 12):
     torch, nn, F = _torch()
 
@@ -94,6 +126,17 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             h = _lin(self.fc1, self.ln2(x))
             h = h * torch.sigmoid(1.702 * h) if self.quick_gelu else F.gelu(h)
             return x + _lin(self.fc2, h)
+
+        def forward_fused(self, x, delta):
+            """The same block on the fused kernels: x (fp32 residual, updated in place) first takes
+            the previous block's bf16 output `delta`; returns this block's bf16 output."""
+            b, n, c = x.shape
+            qkv = _lin(self.qkv, _add_ln(x, delta, self.ln1)).view(b, n, 3, self.heads, c // self.heads)
+            q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
+            a = F.scaled_dot_product_attention(q, k, v)
+            h = _lin(self.fc1, _add_ln(x, _lin(self.proj, a.transpose(1, 2).reshape(b, n, c)), self.ln2))
+            h = _quick_gelu_(h) if self.quick_gelu else F.gelu(h)
+            return _lin(self.fc2, h)
 
     class ViT(nn.Module):
         """ViT-B/16 tower; `out_dim` adds a CLIP-style projection of the CLS token."""
@@ -129,6 +172,13 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
                 x = x.float()
             x = torch.cat([self.cls.expand(x.shape[0], -1, -1), x], 1) + self.pos
             x = self.ln_pre(x)
+            if getattr(self, "fused", False):
+                x = x.contiguous()
+                delta = None
+                for blk in self.blocks:
+                    delta = blk.forward_fused(x, delta)
+                x = self.ln_post(x[:, 0] + delta[:, 0].float())
+                return x if isinstance(self.head, nn.Identity) else _lin(self.head, x)
             for blk in self.blocks:
                 x = blk(x)
             x = self.ln_post(x[:, 0])
@@ -150,9 +200,13 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             parts = [F.normalize(t(x).float(), dim=-1) for t in self.towers]
             return torch.cat(parts, -1)
 
-        def prepare_inference(self, dtype):
+        def prepare_inference(self, dtype, fused=False):
             """Cache low-precision copies of every matrix-product weight once (autocast would
-            re-cast them on every forward); LayerNorms and the residual stream stay fp32."""
+            re-cast them on every forward); LayerNorms and the residual stream stay fp32.
+            fused (bf16, on a GPU): residual add + LayerNorm + bf16 cast and QuickGELU run as
+            single HIP passes (include/imgrec_vit.h)."""
+            for t in self.towers:
+                t.fused = bool(fused) and dtype == torch.bfloat16
             for m in self.modules():
                 if isinstance(m, (nn.Linear, nn.Conv2d)):
                     w = m.weight.detach()
@@ -242,8 +296,8 @@ class DreamSimVectorIndexer(BaseVectorIndexer):
             raise RuntimeError("DreamSim ensemble weights are not available (the reference "
                                "downloads them at run time; pass weights_path=...)")
         self.model = model.to(self.device).eval()
-        if self.device.type == "cuda":
-            self.model.prepare_inference(torch.bfloat16)
+        if self.device.type == "cuda":       # bf16 products + the fused HIP elementwise passes
+            self.model.prepare_inference(torch.bfloat16, fused=True)
         self.dim = model.dim
         self._log_and_print("DreamSim model loaded and warmed up.", level="info")
 
@@ -251,7 +305,8 @@ class DreamSimVectorIndexer(BaseVectorIndexer):
         """(B, 3, 224, 224) float tensor in [0, 1] on the model device -> (B, 1792) normalised.
         On the GPU the matrix products run in bf16 from weights cast once (prepare_inference),
         LayerNorm and the residual stream in fp32 — what autocast does, without re-casting every
-        weight on every forward."""
+        weight on every forward — with the residual add + LayerNorm + bf16 cast and QuickGELU as
+        single HIP passes (include/imgrec_vit.h)."""
         torch, _, F = _torch()
         with torch.no_grad():
             emb = self.model.embed(images)

@@ -1,0 +1,34 @@
+/*
+ * imgrec_vit.h — C ABI of the fused elementwise kernels of the DreamSim-architecture ViT forward
+ * (image_recommender_amd/vector_scripts/create_dreamsim_vector.py).  The reference embeds images
+ * with dreamsim's three ViT-B/16 towers (/root/reference/vector_scripts/create_dreamsim_vector.py:
+ * 38-43, 51-93, `model.embed`); between the bf16 matrix products of every block the forward keeps
+ * an fp32 residual stream and fp32 LayerNorms.  These kernels fuse what would otherwise be
+ * separate passes over the activations.
+ *
+ * bf16 values are raw 16-bit patterns (uint16_t); device pointers; enqueued on `stream`
+ * (hipStream_t, NULL = default stream), no synchronisation.  Return 0, or -1 on bad arguments.
+ */
+#ifndef IMGREC_VIT_H
+#define IMGREC_VIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Per row r of `rows` (row length dim <= 1024): x[r] += delta[r] (bf16, when delta != NULL;
+ * x is updated in place), then y[r] = bf16(LayerNorm(x[r]) * gamma + beta) with the biased
+ * variance and `eps` (torch.nn.LayerNorm semantics, fp32 arithmetic). */
+int vit_add_layernorm_bf16(float* x, const uint16_t* delta, const float* gamma, const float* beta,
+                           uint16_t* y, int64_t rows, int dim, float eps, void* stream);
+
+/* In place on n bf16 values: h = bf16(h * sigmoid(1.702 h)) (CLIP's QuickGELU), fp32 inside. */
+int vit_quick_gelu_bf16(uint16_t* h, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IMGREC_VIT_H */
