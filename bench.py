@@ -142,22 +142,34 @@ def exact_ground_truth(torch, dist, world, cfg, centres, r0, r1, q, k, device, s
     return best_d.cpu().numpy(), best_i.cpu().numpy()
 
 
-def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
-    """Rank 0, N=1 only: the CPU comparator, timed on the FULL corpus of the workload.
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s, nq=1024):
+    """Rank 0, N=1 only: the CPU comparator, timed on the FULL corpus at the GPU's batch size.
 
     faiss-cpu (the reference's library, north_star's HNSW comparator) is not installed on this
-    image, so the comparator is the oracle's restatement of faiss IndexFlatL2's own BLAS search
-    (oracle.flat_knn.search_blas_fp32: norms + sgemm + partial sort per call, as faiss's
-    exhaustive_L2sqr_blas, on numpy's multithreaded BLAS).  The bounded sample is in queries, not
-    rows: batches of the same queries against all N rows until about budget_s of CPU work.
+    image, so the comparator is the oracle's restatement of faiss IndexFlatL2's own search at a
+    large batch (oracle.flat_knn.search_blas_fp32_blocked: exhaustive_L2sqr_blas's corpus blocks,
+    one sgemm of the whole query batch per block on numpy's multithreaded BLAS, per-query top-k
+    folded on a thread pool).  The sample: whole batches of the same `nq` queries the GPU step
+    searches, against all N rows, until about budget_s of CPU work (at least one batch).
     """
-    from oracle.flat_knn import search_blas_fp32
+    from oracle.flat_knn import search_blas_fp32_blocked
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     try:
         from threadpoolctl import threadpool_info
-        cores = max([p.get("num_threads", 1) for p in threadpool_info()
-                     if p.get("user_api") == "blas"] or [os.cpu_count() or 1])
+        blas = max([p.get("num_threads", 1) for p in threadpool_info()
+                    if p.get("user_api") == "blas"] or [threads])
     except Exception:
-        cores = os.cpu_count() or 1
+        blas = threads
     dev = "cuda"
     n, d = D["rows"], int(sum(cfg["parts"]))
     xb = np.empty((n, d), np.float32)
@@ -165,26 +177,25 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s):
     for blk in gen_rows(torch, cfg, centres, 0, n, dev, seed):
         xb[pos:pos + blk.shape[0]] = blk.cpu().numpy()
         pos += blk.shape[0]
-    xq = gen_queries(torch, cfg, centres, 256, dev, seed).cpu().numpy()
-    search_blas_fp32(xb[:65536], xq[:8], k)         # warm BLAS threads
-    t0 = time.perf_counter()
-    search_blas_fp32(xb, xq[:16], k)
-    t_probe = time.perf_counter() - t0
-    nq = int(min(256, max(16, 16 * budget_s / 3 / max(t_probe, 1e-9))))
+    xq = gen_queries(torch, cfg, centres, nq, dev, seed).cpu().numpy()
+    search_blas_fp32_blocked(xb[:65536], xq, k, threads=threads)     # warm BLAS threads + pool
     times = []
     t_start = time.perf_counter()
     while True:
         t0 = time.perf_counter()
-        search_blas_fp32(xb, xq[:nq], k)
+        search_blas_fp32_blocked(xb, xq, k, threads=threads)
         times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > budget_s or len(times) >= 10:
+        if time.perf_counter() - t_start > budget_s or len(times) >= 5:
             break
     t = float(np.median(times))
     return {
-        "value": nq / t, "unit": "queries/s", "cores": int(cores), "kind": "port",
-        "sample": (f"all {n} rows x {d} of the workload's corpus, {nq} of its queries per batch, "
-                   f"median of {len(times)} batches; oracle.flat_knn.search_blas_fp32 = faiss "
-                   f"exhaustive_L2sqr_blas restated (faiss-cpu absent on the box)"),
+        "value": nq / t, "unit": "queries/s", "cores": int(max(blas, threads)), "kind": "port",
+        "cpu_model": cpu_model(), "blas_threads": int(blas), "topk_threads": int(threads),
+        "sample": (f"all {n} rows x {d} of the workload's corpus, {nq} queries per batch (the GPU "
+                   f"step's batch), median of {len(times)} batches of {t:.2f} s; "
+                   f"oracle.flat_knn.search_blas_fp32_blocked = faiss IndexFlatL2 "
+                   f"exhaustive_L2sqr_blas restated (65536-row corpus blocks, one sgemm per block, "
+                   f"threaded per-query top-k); faiss-cpu absent on the box"),
     }
 
 
@@ -258,15 +269,25 @@ def main():
     # IMGREC_DIST_BACKEND=gloo rehearses the N-rank protocol with every rank on one visible GPU
     # (local % device count); the measured runs use RCCL ("nccl"), one rank per GPU
     backend = os.environ.get("IMGREC_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and (ndev < world or local >= ndev):
+        # one rank per GPU over RCCL: fail at once, before any collective could hang
+        raise SystemExit(f"[bench] rank {rank}: WORLD_SIZE={world} ranks need {world} visible GPUs, "
+                         f"this process sees {ndev} (LOCAL_RANK={local})")
     if backend != "nccl":
-        local = local % max(torch.cuda.device_count(), 1)
+        local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
+        from datetime import timedelta
+        # a rank that never arrives ends the run with an error after this long instead of hanging
+        tmo = timedelta(seconds=float(os.environ.get("IMGREC_DIST_TIMEOUT_S", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
+        dist.barrier()           # every rank up (and the RCCL communicator formed) before any work
+        print(f"[bench] rank {rank}/{world}: {backend} up on cuda:{local}", file=sys.stderr, flush=True)
 
     from image_recommender_amd import _lib
     from image_recommender_amd.faiss_compat import METRIC_L2
@@ -294,33 +315,52 @@ def main():
     def step():
         return shard.search(q, a.k)
 
+    import ctypes as C
+    h = shard.index.handle
+
+    def region(fn, steps, kernel_events):
+        """Run fn `steps` times between barrier + synchronize on both sides -> (max-over-ranks wall
+        seconds, average candidate-kernel ms or None, last output).  kernel_events: the library
+        records a HIP event pair around every candidate-kernel launch on its launch stream
+        (knn_set_timing).  Each event costs ~5.7 us of GPU time (an idle gap before the next
+        kernel, profiles/r03/), so the throughput region records none; the kernel duration comes
+        from a second region of the same steps."""
+        if kernel_events:
+            lib.knn_set_timing(h, 1)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(steps):
+            out = fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        kms = 0.0
+        if kernel_events:
+            tot_ms, nl = C.c_double(), C.c_int()
+            _lib.check(lib.knn_kernel_time(h, C.byref(tot_ms), C.byref(nl)), "timing")
+            lib.knn_set_timing(h, 0)
+            kms = tot_ms.value / max(nl.value, 1)
+        v = torch.tensor([el, kms], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        return float(v[0]), (float(v[1]) if kernel_events else None), out
+
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    lib.knn_set_timing(shard.index.handle, 1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        Dr, Ir = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, _, (Dr, Ir) = region(step, a.steps, False)          # the bench value
     split_q, fallback_q, err_ratio = shard.index.search_stats(with_error=True)   # last step
-    path = lib.knn_last_path(shard.index.handle)          # 0 exact, 1 split, 2 bf16
-    import ctypes as C
-    tot_ms, nl = C.c_double(), C.c_int()
-    _lib.check(lib.knn_kernel_time(shard.index.handle, C.byref(tot_ms), C.byref(nl)), "timing")
-    lib.knn_set_timing(shard.index.handle, 0)
-    el = torch.tensor([elapsed, tot_ms.value / max(nl.value, 1)], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(el[0]), float(el[1])
+    path = lib.knn_last_path(h)                                # 0 exact, 1 split, 2 bf16
+    kel, kern_ms, _ = region(step, a.steps, True)               # candidate-kernel duration
     if a.profile_only:
         if rank == 0:
-            print(json.dumps({"elapsed_s": elapsed, "kernel_ms": kern_ms, "split_queries": split_q,
+            print(json.dumps({"elapsed_s": elapsed, "ms_per_step": elapsed / a.steps * 1e3,
+                              "ms_per_step_with_kernel_events": kel / a.steps * 1e3,
+                              "kernel_ms": kern_ms, "split_queries": split_q,
                               "fallback_queries": fallback_q, "err_ratio": err_ratio}))
         if world > 1:
             dist.destroy_process_group()
@@ -341,28 +381,16 @@ def main():
     for _ in range(3):
         shard.search(q1, a.k)
     torch.cuda.synchronize()
-    lib.knn_set_timing(shard.index.handle, 1)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    for _ in range(a.single_query_steps):
-        shard.search(q1, a.k)
-    torch.cuda.synchronize()
-    el1 = time.perf_counter() - t1
-    _lib.check(lib.knn_kernel_time(shard.index.handle, C.byref(tot_ms), C.byref(nl)), "timing")
-    lib.knn_set_timing(shard.index.handle, 0)
-    e1 = torch.tensor([el1, tot_ms.value / max(nl.value, 1)], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(e1, op=dist.ReduceOp.MAX)
-    el1, kern1_ms = float(e1[0]), float(e1[1])
-    path1 = lib.knn_last_path(shard.index.handle)          # 0 exact, 1 split, 2 bf16
+    el1, _, _ = region(lambda: shard.search(q1, a.k), a.single_query_steps, False)
+    _, kern1_ms, _ = region(lambda: shard.search(q1, a.k), a.single_query_steps, True)
+    path1 = lib.knn_last_path(h)                               # 0 exact, 1 split, 2 bf16
 
     tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
     lib.knn_plan(shard.index.handle, nq_local, a.k, C.byref(tr), C.byref(tq), C.byref(sp), C.byref(wg))
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(torch, cfg, centres, {"rows": cfg["rows"]}, a.k, seed, a.cpu_seconds)
+        cpu = cpu_baseline(torch, cfg, centres, {"rows": cfg["rows"]}, a.k, seed, a.cpu_seconds, a.nq)
 
     if rank == 0:
         n_local = shard.local_rows
@@ -430,6 +458,8 @@ def main():
                 "traffic_source": traffic[1] if traffic else None,
                 "kernel": kname,
                 "kernel_ms": kern_ms,
+                "kernel_timing": (f"HIP events around each launch on its stream, a second region "
+                                  f"of {a.steps} steps (the value region records no events)"),
                 "mfma_busy": busy[0]["mfma_busy"] if busy else None,
                 "clock_ghz": busy[0]["clock_ghz"] if busy else None,
                 "busy_source": busy[1] if busy else None,

@@ -7,8 +7,8 @@
 //
 // Stream semantics: *_device entry points enqueue on the caller's stream and return without
 // waiting for the GPU; host-pointer entry points run on the index's own stream and synchronise.
-// Every operation records the index's fence event on its stream, and an operation on another
-// stream waits for it first, so mixing streams (or host and device calls) is always ordered.
+// An operation on another stream than the previous one first waits for the previous one's stream
+// (fence_begin), so mixing streams (or host and device calls) is always ordered.
 
 #include <cstdarg>
 #include <cstdio>
@@ -34,13 +34,23 @@ void set_err(const char* fmt, ...) {
 
 const char* last_error() { return g_err.c_str(); }
 
+// The fence is recorded lazily: an operation only remembers its stream, and the event is
+// recorded on that stream when (and only when) a later operation arrives on a different one.  The
+// event then marks the stream's current tail, which includes every earlier operation on the index
+// (and possibly later unrelated work of the caller: a conservative, still correct wait).  A stream
+// that never changes pays nothing — an event record costs ~5.7 us of GPU time per call on MI355X
+// (the gap it leaves between the kernels around it, profiles/r03/), more than the near-empty
+// kernels of a search.  The stream of an operation must therefore stay valid until the next
+// operation on the index is enqueued (include/imgrec_knn.h, Conventions).
 int fence_begin(knn_index* ix, hipStream_t st) {
-    if (ix->fence_set && ix->fence_stream != st) KNN_HIP(hipStreamWaitEvent(st, ix->fence, 0));
+    if (ix->fence_set && ix->fence_stream != st) {
+        KNN_HIP(hipEventRecord(ix->fence, ix->fence_stream));
+        KNN_HIP(hipStreamWaitEvent(st, ix->fence, 0));
+    }
     return KNN_OK;
 }
 
 int fence_end(knn_index* ix, hipStream_t st) {
-    KNN_HIP(hipEventRecord(ix->fence, st));
     ix->fence_stream = st;
     ix->fence_set = true;
     return KNN_OK;
@@ -63,7 +73,8 @@ int reserve_rows(knn_index* ix, int64_t need, hipStream_t st) {
     };
     hipError_t e = hipMalloc((void**)&nxb, (size_t)ncap * ix->dp * sizeof(float));
     if (e == hipSuccess) e = hipMalloc((void**)&nxn, (size_t)ncap * sizeof(float));
-    if (e == hipSuccess && ix->split_ok) e = hipMalloc((void**)&nxs, (size_t)ncap * ix->dp * sizeof(uint32_t));
+    // the split copy exists only once a split-mode search has materialised it (ensure_split)
+    if (e == hipSuccess && ix->xs) e = hipMalloc((void**)&nxs, (size_t)ncap * ix->dp * sizeof(uint32_t));
     if (e == hipSuccess && ix->b16_ok) e = hipMalloc((void**)&nxh, (size_t)ncap * ix->dpb * sizeof(uint16_t));
     if (e == hipSuccess && ix->b16_ok) e = hipMalloc((void**)&nxr, (size_t)ncap * sizeof(float));
     if (e != hipSuccess) {
@@ -108,7 +119,7 @@ int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st) 
     if (rc != KNN_OK) return rc;
     KNN_HIP(launch_rows_ingest(x, n, ix->d, ix->dp, n, ix->metric == KNN_METRIC_COSINE ? 1 : 0,
                                ix->xb + (size_t)ix->ntotal * ix->dp, ix->xn + ix->ntotal, st));
-    if (ix->split_ok)
+    if (ix->xs)
         KNN_HIP(launch_split_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp, kSplitBK,
                                   ix->xs + (size_t)ix->ntotal * ix->dp, st));
     if (ix->b16_ok)
@@ -116,6 +127,24 @@ int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st) 
                                  ix->xh + (size_t)ix->ntotal * ix->dpb, ix->xr + ix->ntotal, st));
     ix->ntotal += n;
     ix->xn_max_stale = true;
+    return KNN_OK;
+}
+
+// The split-bf16 copy (cap x dp words, as many bytes as the fp32 rows) is built on the first
+// search that runs the split path, from the stored fp32 rows, and kept up to date by later adds.
+// AUTO never takes the split path while the bf16 copy exists (every d >= 64), so a default index
+// holds only the fp32 rows, norms and the bf16 copy: 12 GB instead of 20 GB per 1M x 1968 rows.
+int ensure_split(knn_index* ix, hipStream_t st) {
+    if (ix->xs) return KNN_OK;
+    if (!ix->split_ok) KNN_FAIL(KNN_EINVAL, "split search needs d >= 256; d = %d", ix->d);
+    uint32_t* xs = nullptr;
+    if (hipMalloc((void**)&xs, (size_t)std::max<int64_t>(ix->cap, 1) * ix->dp * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        KNN_FAIL(KNN_ENOMEM, "hipMalloc of the %lld-row split copy failed", (long long)ix->cap);
+    }
+    ix->xs = xs;
+    if (ix->ntotal > 0)
+        KNN_HIP(launch_split_rows(ix->xb, ix->ntotal, ix->dp, kSplitBK, ix->xs, st));
     return KNN_OK;
 }
 

@@ -92,7 +92,7 @@ struct knn_index {
     bool trained = true;
     float* xb = nullptr;     // cap x dp
     float* xn = nullptr;     // cap
-    uint32_t* xs = nullptr;  // cap x dp split-bf16 copy (split_ok only)
+    uint32_t* xs = nullptr;  // cap x dp split-bf16 copy (built by the first split search)
     uint16_t* xh = nullptr;  // cap x dpb bf16 copy (b16_ok only)
     float* xr = nullptr;     // cap: |x - bf16(x)| per row (b16_ok only)
     float* xn_max = nullptr; // device scalar, max |x|^2 (refreshed when rows change)
@@ -104,9 +104,9 @@ struct knn_index {
     int64_t last_split_queries = 0;   // queries of the last search on a candidate path
     hipStream_t stream = nullptr;     // the index's own stream (host-pointer entry points)
     std::mutex mu;
-    // Cross-stream ordering: every operation enqueued on the index records `fence` on its stream;
-    // an operation on a different stream first waits for it (adds before searches, one search's
-    // workspace use before the next's, ...).
+    // Cross-stream ordering: every operation enqueued on the index remembers its stream; an
+    // operation on a different stream first records `fence` on the remembered stream and waits
+    // for it (adds before searches, one search's workspace use before the next's, ...).
     hipEvent_t fence = nullptr;
     hipStream_t fence_stream = nullptr;
     bool fence_set = false;
@@ -163,6 +163,7 @@ int fence_begin(knn_index* ix, hipStream_t st);
 int fence_end(knn_index* ix, hipStream_t st);
 int reserve_rows(knn_index* ix, int64_t need, hipStream_t st);
 int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st);
+int ensure_split(knn_index* ix, hipStream_t st);
 int create_single(int d, int metric, int device, knn_index** out);
 void free_single(knn_index* ix);
 // knn_search.cpp

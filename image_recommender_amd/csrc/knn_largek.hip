@@ -243,10 +243,19 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         return KNN_OK;
     }
     int rc;
-    if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq * ix->dp)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq)) != KNN_OK) return rc;
-    KNN_HIP(launch_rows_ingest(q, nq, ix->d, ix->dp, nq, ix->metric == KNN_METRIC_COSINE ? 1 : 0,
-                               ix->qpad, ix->qnorm, st));
+    // Small batches: S stripes of running lists per query, so one GEMM round covers S corpus
+    // blocks (S x fewer GEMM + select launches, S workgroups per query) and a final kernel merges
+    // the S lists (S * k <= kLKM).  Large batches fill the chip with one stripe.
+    const int S = nq <= 64 ? (int)std::max<int64_t>(1, std::min<int64_t>(32, kLKM / k)) : 1;
+    const int64_t nqc = std::min<int64_t>(nq, 2048);       // queries per GEMM block
+    const int nrc_max = kLKM - k;
+    const int64_t round_rows = (int64_t)S * nrc_max;
+    // workspace sized for ONE query block (queries, norms, GEMM block, running lists), reused
+    // by every block: independent of the batch size
+    if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nqc * ix->dp)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nqc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->lk_g, &ix->lk_g_cap, (size_t)nqc * round_rows)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)S * nqc * k)) != KNN_OK) return rc;
     if (!ix->blas) {
         rocblas_handle h;
         if (rocblas_create_handle(&h) != rocblas_status_success)
@@ -255,34 +264,29 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     }
     const rocblas_handle h = (rocblas_handle)ix->blas;
     if (rocblas_set_stream(h, st) != rocblas_status_success) KNN_FAIL(KNN_EHIP, "rocblas_set_stream failed");
-    const int nrc_max = kLKM - k;
-    // Small batches: S stripes of running lists per query, so one GEMM round covers S corpus
-    // blocks (S x fewer GEMM + select launches, S workgroups per query) and a final kernel merges
-    // the S lists (S * k <= kLKM).  Large batches fill the chip with one stripe.
-    const int S = nq <= 64 ? (int)std::max<int64_t>(1, std::min<int64_t>(32, kLKM / k)) : 1;
-    const int64_t nqc = std::min<int64_t>(nq, 2048);
-    const int64_t round_rows = (int64_t)S * nrc_max;
-    if ((rc = grow(&ix->lk_g, &ix->lk_g_cap, (size_t)nqc * round_rows)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)S * nq * k)) != KNN_OK) return rc;
     const float alpha = -2.f, beta = 0.f;
     for (int64_t q0 = 0; q0 < nq; q0 += nqc) {
         const int qc = (int)std::min<int64_t>(nqc, nq - q0);
+        KNN_HIP(launch_rows_ingest(q + q0 * ix->d, qc, ix->d, ix->dp, qc,
+                                   ix->metric == KNN_METRIC_COSINE ? 1 : 0, ix->qpad, ix->qnorm, st));
+        float* Db = D + q0 * k;          // the block's outputs; the kernels index it from 0
+        int64_t* Ib = I + q0 * k;
         for (int64_t r0 = 0; r0 < ix->ntotal; r0 += round_rows) {
             const int m = (int)std::min<int64_t>(round_rows, ix->ntotal - r0);
             // column-major: G (m x qc, ld m) = X_rows^T (m x dp) * Q_block (dp x qc)
             if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, m, qc, ix->dp,
-                              &alpha, ix->xb + r0 * ix->dp, ix->dp, ix->qpad + q0 * ix->dp, ix->dp,
+                              &alpha, ix->xb + r0 * ix->dp, ix->dp, ix->qpad, ix->dp,
                               &beta, ix->lk_g, m) != rocblas_status_success)
                 KNN_FAIL(KNN_EHIP, "rocblas_sgemm failed");
             const int last = (S == 1 && r0 + m >= ix->ntotal) ? 1 : 0;
             hipLaunchKernelGGL(largek_select_kernel, dim3((unsigned)qc, (unsigned)S), dim3(kLKThreads), 0, st,
                                ix->lk_g, m, nrc_max, ix->qnorm, ix->xn, r0, k, kmetric, r0 == 0 ? 1 : 0,
-                               last, q0, nq, ix->lk_run, D, I, ix->id_offset);
+                               last, (int64_t)0, nqc, ix->lk_run, Db, Ib, ix->id_offset);
             KNN_HIP(hipGetLastError());
         }
         if (S > 1) {
             hipLaunchKernelGGL(largek_final_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st,
-                               ix->lk_run, S, nq, k, q0, kmetric, D, I, ix->id_offset);
+                               ix->lk_run, S, nqc, k, (int64_t)0, kmetric, Db, Ib, ix->id_offset);
             KNN_HIP(hipGetLastError());
         }
     }

@@ -203,6 +203,7 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
     const int kc = split_kc(k);
     const Plan p = make_split_plan(ix->ntotal, nq, kc, ix->cus);
     int rc;
+    if ((rc = ensure_split(ix, st)) != KNN_OK) return rc;
     if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
     if ((rc = grow(&ix->qsplit, &ix->qsplit_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;

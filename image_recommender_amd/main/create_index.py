@@ -29,6 +29,7 @@ import logging
 import os
 import sqlite3
 from pathlib import Path
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -136,9 +137,11 @@ class FAISSIndexBuilderDB:
 
     def _initialize_index(self, dim, use_pq=True):
         if use_pq:
-            coarse = faiss.IndexHNSWFlat(dim, self.hnsw_M, device=self.device)
-            coarse.hnsw.efConstruction = self.efConstruction
-            coarse.hnsw.efSearch = self.efSearch
+            # the reference's IndexHNSWFlat(dim, 32) coarse quantiser (create_index.py:219-221) is
+            # recorded as parameters only: the exact index never consults it, so no second device
+            # index is created for it
+            coarse = SimpleNamespace(d=dim, hnsw=SimpleNamespace(
+                M=self.hnsw_M, efConstruction=self.efConstruction, efSearch=self.efSearch))
             nlist, m, nbits = 2048, self.find_valid_m(dim), 12
             index = faiss.IndexIVFPQ(coarse, dim, nlist, m, nbits, device=self.device)
             self._log(f"Created exact MI355X flat index behind the IVFPQ interface "

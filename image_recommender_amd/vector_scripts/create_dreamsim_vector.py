@@ -78,8 +78,18 @@ def _add_ln(x, delta, ln):
     import torch
     from .. import _lib
     c = x.shape[-1]
+    if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()):
+        raise TypeError("_add_ln: x must be a contiguous fp32 GPU tensor (updated in place)")
+    if ln.weight.dtype != torch.float32 or ln.bias.dtype != torch.float32:
+        raise TypeError("_add_ln: LayerNorm parameters must be fp32")
+    if delta is not None:
+        # kept alive in this frame until the kernel is enqueued (a temporary's storage could be
+        # reused by the caching allocator before the launch)
+        delta = delta.contiguous()
+        if delta.dtype != torch.bfloat16 or delta.shape != x.shape:
+            raise TypeError("_add_ln: delta must be bf16 with x's shape")
     y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-    d = 0 if delta is None else delta.contiguous().data_ptr()
+    d = 0 if delta is None else delta.data_ptr()
     rc = _lib.load().vit_add_layernorm_bf16(
         C.c_void_p(x.data_ptr()), C.c_void_p(d), C.c_void_p(ln.weight.data_ptr()),
         C.c_void_p(ln.bias.data_ptr()), C.c_void_p(y.data_ptr()), x.numel() // c, c, float(ln.eps),

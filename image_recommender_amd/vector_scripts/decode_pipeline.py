@@ -6,7 +6,7 @@ The reference decodes every image with ``cv2.imread`` + ``cvtColor`` in a
 /root/reference/vector_scripts/create_vector_base.py:242-247).  Here the CPU does only what it
 must — the decode — and the histogram runs on the GPU, with the two overlapped:
 
-* worker processes (fork, started before any GPU work of this object) decode chunks of images with
+* worker processes (from a forkserver, so independent of this process's GPU state) decode chunks of images with
   PIL straight into slots of ONE shared-memory ring; a slot holds a chunk's RGB bytes back to back
   (each image 48-byte aligned, so the HIP kernel's pixel-phase fast path applies) and, at its end,
   the chunk's image offsets and pixel counts;
@@ -38,6 +38,13 @@ _ALIGN = 48              # 16-B aligned and a whole number of pixels
 _W = {}                  # worker-side state (set by _attach in each worker process)
 
 
+def _pix_cap(slot_bytes: int, meta_cap: int) -> int:
+    """Pixel bytes of a slot: what precedes its meta block, rounded down to a multiple of _ALIGN
+    (an image placed at an aligned offset that fits ends within it, and so does the rounded
+    offset after it)."""
+    return (slot_bytes - 16 * meta_cap) // _ALIGN * _ALIGN
+
+
 def _attach(shm_name: str, slot_bytes: int, meta_cap: int):
     _W["shm"] = shared_memory.SharedMemory(name=shm_name)
     _W["slot_bytes"] = slot_bytes
@@ -56,12 +63,12 @@ def _decode_chunk(args):
     -1 unreadable / wrong shape, -2 spilled (did not fit the slot: returned as an array)."""
     slot, paths = args
     shm, sb, mc = _W["shm"], _W["slot_bytes"], _W["meta_cap"]
-    pix_cap = sb - 16 * mc
+    pix_cap = _pix_cap(sb, mc)
     base = slot * sb
     buf = np.ndarray((sb,), dtype=np.uint8, buffer=shm.buf, offset=base)
-    meta = np.ndarray((2 * mc,), dtype=np.int64, buffer=shm.buf, offset=base + pix_cap)
+    meta = np.ndarray((2 * mc,), dtype=np.int64, buffer=shm.buf, offset=base + sb - 16 * mc)
     offs, npix = [], []
-    off, n, status, spill = 0, 0, [], {}
+    off, end, n, status, spill = 0, 0, 0, [], {}
     for i, p in enumerate(paths):
         img = load_image(p, normalize=False, as_array=True)
         if img is None or img.ndim != 3 or img.shape[2] != 3 or img.dtype != np.uint8:
@@ -77,10 +84,11 @@ def _decode_chunk(args):
         npix.append(img.shape[0] * img.shape[1])
         status.append(n)
         n += 1
+        end = off + nb                            # bytes the upload must move (<= pix_cap)
         off += (nb + _ALIGN - 1) // _ALIGN * _ALIGN
     meta[:n] = offs                               # [n offsets | n pixel counts], compact
     meta[n:2 * n] = npix
-    return slot, status, off, n, spill
+    return slot, status, end, n, spill
 
 
 class ColorDecodePipeline:
@@ -102,12 +110,13 @@ class ColorDecodePipeline:
         self.meta_cap = self.chunk
         self.lib = _lib.load()
         self.shm = shared_memory.SharedMemory(create=True, size=self.nslots * self.slot_bytes)
-        # the workers are forked now, before this object touches the GPU; they never use it
-        self.pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("fork"),
+        # the workers come from a forkserver (a fresh interpreter that never touches HIP), so they
+        # are safe to start whatever GPU state this process is in; they never use the GPU
+        self.pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("forkserver"),
                                         initializer=_attach,
                                         initargs=(self.shm.name, self.slot_bytes, self.meta_cap))
-        # every worker must exist now (an on-demand fork would come after the GPU is in use):
-        # each holds a task until all have started
+        # start every worker now (not on demand inside the decode loop): each holds a task until
+        # all have started
         list(self.pool.map(_hold, [0.3] * self.workers))
         self.base = C.addressof(C.c_char.from_buffer(self.shm.buf))
         rc = self.lib.color_host_register(C.c_void_p(self.base), self.nslots * self.slot_bytes)
@@ -118,7 +127,7 @@ class ColorDecodePipeline:
         dev = torch.cuda.current_device() if device is None else device
         self.device = torch.device("cuda", dev)
         self.stream = torch.cuda.Stream(device=self.device)
-        pix_cap = self.slot_bytes - 16 * self.meta_cap
+        pix_cap = _pix_cap(self.slot_bytes, self.meta_cap)
         self.dev_pix = [torch.empty(pix_cap, dtype=torch.uint8, device=self.device) for _ in range(2)]
         self.dev_meta = [torch.empty(2 * self.meta_cap, dtype=torch.int64, device=self.device)
                          for _ in range(2)]

@@ -32,11 +32,14 @@
  *     candidate paths' certificate, its second chance and the exact re-run of the queries it
  *     cannot settle are all decided on the device.  They allocate only when the workspace must
  *     grow.
- *   - Operations on one index may come from different streams and threads: each records an
- *     event on its stream and an operation on another stream waits for the previous one's first
- *     (an add on stream A is complete before a search on stream B reads the rows; two searches
- *     never share the workspace concurrently).  A call on the index's host entry points is
- *     ordered after earlier device-stream calls the same way.
+ *   - Operations on one index may come from different streams and threads: an operation on
+ *     another stream than the previous operation's first waits for that stream (an add on stream
+ *     A is complete before a search on stream B reads the rows; two searches never share the
+ *     workspace concurrently).  A call on the index's host entry points is ordered after earlier
+ *     device-stream calls the same way.  The wait is set up when the stream changes (an event
+ *     recorded then on the previous stream), so the stream of an operation must stay valid until
+ *     the next operation on the index is enqueued; back-to-back operations on one stream record
+ *     no event at all.
  *   - Vectors are row-major float32, n rows × d.  Labels are int64.  Result rows are sorted by
  *     ascending distance (L2) or descending inner product (IP/COSINE); exact ties are broken by the
  *     smaller label.  When fewer than k vectors exist, the tail of a result row holds label -1 and
@@ -73,11 +76,14 @@ enum knn_error {
 /* Search arithmetic.  Every mode returns the exact search's result up to the fp32 tie window:
  * a candidate pass proposes K' rows per query, an fp32 rerank computes their exact keys and a
  * per-query error-bound certificate proves that no row outside the candidates can rank before a
- * returned one.  The returned labels are those of the fp32 keys of the rerank, so they equal the
- * EXACT mode's labels wherever consecutive keys differ by more than the fp32 evaluation error of
- * the two summation orders (the rerank's FMA chain vs the MFMA chain: ~1e-6 relative); inside such
- * a tie window two modes may order near-equal rows differently, never return a row whose exact
- * distance is farther than the bound.  A query whose certificate fails gets a second chance (every
+ * returned one.  The returned labels are those of the fp32 keys of the rerank.  Tie window, as
+ * tested (tests/knn_check.py): labels equal the float64 oracle's at every rank whose exact distance
+ * is separated from both neighbours by more than twice the rigorous fp32 bound
+ * gamma_D (|q|^2 + |x|^2 + 2 sum|q_i x_i|) + rounding of the norm terms (gamma_D = D u / (1 - D u),
+ * u = 2^-24: about 1e-4 relative at D = 1968); inside that window modes may order near-equal rows
+ * differently, and every returned distance is within the bound of its row's exact distance.  The
+ * observed fp32 disagreement of two summation orders is far smaller (~1e-7 relative on the bench
+ * data), but only the rigorous window is a promise.  A query whose certificate fails gets a second chance (every
  * per-split list entry reranked, certified against the list floor); if that fails too it is
  * re-run on the exact fp32 kernel, planned on the device.
  * AUTO: the bf16 path (d >= 64; one bf16 MFMA per product, K' = 64) for batches of > 128
@@ -96,8 +102,9 @@ enum knn_search_mode {
 /* Largest k the fused top-k kernels serve (they keep per-lane lists of this length). */
 #define KNN_MAX_K 32
 /* Largest k one search can return: KNN_MAX_K < k <= KNN_MAX_K_LARGE runs faiss IndexFlat's own
- * algorithm (fp32 GEMM blocks + an exact per-query radix select, csrc/knn_largek.hip) on a
- * single-device index; a multi-device index (knn_create_multi) serves k <= KNN_MAX_K. */
+ * algorithm (fp32 GEMM blocks + an exact per-query radix select, csrc/knn_largek.hip); a
+ * multi-device index (knn_create_multi) runs it on every shard and merges the shards' k-lists with
+ * the same select (at most 8192 gathered entries per query). */
 #define KNN_MAX_K_LARGE 1024
 
 /* Create an empty index of dimension d on HIP device `device` (-1 = current device). */

@@ -10,9 +10,11 @@ Contents
   plumbing.py     the reference's index/search plumbing: canonical type order, find_valid_m,
                   query assembly (concat -> mean -> normalize_L2), offset bookkeeping.
   color_hist.py   cv2.calcHist-equivalent RGB histogram + L2 normalisation (numpy bincount).
-  blob.py         the pickle protocol-5 BLOB format of the vector tables.
-  c/              plain-C restatements (flat L2/IP search in double, colour histogram) built by
-                  oracle/c/Makefile into oracle/_build/ (git-ignored).
+  ivfpq.py        faiss IndexIVFPQ's by-residual ADC search (the opt-in IVF-PQ index).
+  c/              plain-C restatements (flat L2/IP search in double, colour histogram counts)
+                  built by oracle/c/Makefile into oracle/_build/liboracle.so (git-ignored);
+                  tests/test_oracle_c_cpu.py holds them against flat_knn.py / color_hist.py, and
+                  the full-size cfg2 GPU test uses the C search as its second, independent checker.
 
 Parity status: the arithmetic of the path lives in faiss-cpu 1.10.0 and
 opencv-python 4.11.0.86, neither installed nor vendored, so it is "parity unpinned" against the

@@ -132,6 +132,50 @@ def search_blas_fp32(xb: np.ndarray, xq: np.ndarray, k: int, xb_norms: np.ndarra
     return np.take_along_axis(pd, order, 1), np.take_along_axis(part, order, 1)
 
 
+def search_blas_fp32_blocked(xb: np.ndarray, xq: np.ndarray, k: int, block: int = 65536,
+                             threads: int | None = None, xb_norms: np.ndarray | None = None):
+    """faiss IndexFlatL2.search at a large batch, restated: exhaustive_L2sqr_blas's corpus blocking
+    (the CPU comparator of bench.py, not a checker).
+
+    faiss (faiss/utils/distances.cpp, exhaustive_L2sqr_blas) walks the corpus in blocks of bs_y
+    rows, runs one sgemm of the whole query block against each corpus block, forms
+    dis = |q|^2 + |x|^2 - 2 ip, and folds every block into per-query heaps with OpenMP over
+    queries.  Here: one sgemm per corpus block (numpy's multithreaded BLAS), then the per-query
+    top-k of the block and its merge with the running top-k by argpartition on `threads` threads
+    (numpy releases the GIL in argpartition).  Returns (D float32, I int64), ascending.
+    """
+    from concurrent.futures import ThreadPoolExecutor
+    import os
+    xq = np.ascontiguousarray(xq, dtype=np.float32)
+    nq, n = xq.shape[0], xb.shape[0]
+    threads = threads or os.cpu_count() or 1
+    qn = (xq * xq).sum(1, dtype=np.float32)
+    best_d = np.full((nq, k), np.inf, np.float32)
+    best_i = np.full((nq, k), -1, np.int64)
+    chunks = [slice(c, min(nq, c + max(1, -(-nq // threads)))) for c in range(0, nq, max(1, -(-nq // threads)))]
+    with ThreadPoolExecutor(threads) as ex:
+        for r0 in range(0, n, block):
+            xc = np.ascontiguousarray(xb[r0:r0 + block], dtype=np.float32)
+            xn = (xc * xc).sum(1, dtype=np.float32) if xb_norms is None else xb_norms[r0:r0 + block]
+            dis = xq @ xc.T
+            dis *= -2.0
+            dis += qn[:, None]
+            dis += xn[None, :]
+            np.maximum(dis, 0, out=dis)
+            kk = min(k, xc.shape[0])
+
+            def fold(s, dis=dis, kk=kk, r0=r0):
+                part = np.argpartition(dis[s], kk - 1, axis=1)[:, :kk]
+                cd = np.concatenate([best_d[s], np.take_along_axis(dis[s], part, 1)], 1)
+                ci = np.concatenate([best_i[s], part + r0], 1)
+                sel = np.argpartition(cd, k - 1, axis=1)[:, :k]
+                best_d[s] = np.take_along_axis(cd, sel, 1)
+                best_i[s] = np.take_along_axis(ci, sel, 1)
+            list(ex.map(fold, chunks))
+    order = np.argsort(best_d, axis=1, kind="stable")
+    return np.take_along_axis(best_d, order, 1), np.take_along_axis(best_i, order, 1)
+
+
 def recall_at_k(I: np.ndarray, I_gt: np.ndarray, k: int) -> float:
     """|I[:, :k] ∩ I_gt[:, :k]| / k averaged over queries (BASELINE.json metric)."""
     hits = 0

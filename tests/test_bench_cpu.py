@@ -44,3 +44,19 @@ def test_committed_records_cover_the_bench_kernel():
     assert src.endswith("_traffic.json") and 5e9 < bytes_ < 7e9     # 1.5x the 3.97 GB bf16 corpus
     rec, src = bench.pmc_record(pat, "_clock.json")
     assert src.endswith("_clock.json") and 0.0 < rec["mfma_busy"] < 1.0
+
+
+def test_cpu_comparator_is_exact_flat_search():
+    """The CPU comparator (faiss exhaustive_L2sqr_blas restated, corpus-blocked, threaded top-k)
+    returns the float64 oracle's neighbours: it is a faithful port, timed by bench.py at the GPU
+    step's 1024-query batch."""
+    import numpy as np
+    from oracle.flat_knn import search_blas_fp32_blocked, search_exact
+    from tests.datagen import concat_rows
+    xb = concat_rows(20000, seed=11)
+    xq = concat_rows(64, seed=12)
+    D, I = search_blas_fp32_blocked(xb, xq, 10, block=4096, threads=4)
+    Dg, Ig = search_exact(xb, xq, 10, "l2")
+    assert (I == Ig).mean() > 0.99           # fp32 near-ties may swap
+    np.testing.assert_allclose(D, Dg, rtol=0, atol=1e-4)
+    assert (np.diff(D, axis=1) >= 0).all()

@@ -213,3 +213,149 @@ def test_cfg5_pipeline_smoke(gpu):
     got = counts.cpu().numpy()
     for i in range(n):
         np.testing.assert_array_equal(got[i], color_counts(host[i], 16))
+
+
+# --------------------------------------------------------------------------------------------
+# cfg2 at its full size
+# --------------------------------------------------------------------------------------------
+_DUP_SRC, _DUP_ROWS = 100_000, [24 + 512 * j for j in range(16)]
+
+
+def test_cfg2_full_size_auto_with_forced_rerun(faiss):
+    """cfg2 (BASELINE.json configs[1]): 1M x 768 DreamSim-only rows, L2, k = 10, 1024 queries on
+    AUTO (the 256 x 256-tile bf16 kernel at d = 768), /root/reference/main/search_from_image.py:247.
+
+    Query 0 is made to need the device-planned exact re-run AT 1M ROWS: it equals corpus row
+    100000, and 16 rows that all sit in ONE row split of the candidate kernel (8-row groups 3,
+    67, 131, ... of the 64 splits) are copies of that row.  Their split's list then holds 10 keys
+    equal to the answer, so the list floor equals the 10th key and neither the first certificate
+    nor the second chance can settle the query: it is re-run on the fp32 kernel, and its answer
+    is the 10 smallest labels among the 17 copies (exact ties by the smaller label).  The sampled
+    queries are checked against the float64 oracle (oracle.flat_knn) and the first eight also
+    against the independent plain-C oracle (oracle/c/oracle_ref.c)."""
+    import torch
+    from image_recommender_amd import _lib
+    from oracle import c_oracle
+    from oracle.flat_knn import search_exact
+    blocks, xb, q = _generate(torch, 2, 0, 1_000_000, NQ)
+    assert xb.shape == (1_000_000, 768)
+    src = xb[_DUP_SRC].copy()
+    xb[_DUP_ROWS] = src
+    blocks[0][_DUP_ROWS] = torch.from_numpy(src).to(blocks[0].device)   # rows < 16384: block 0
+    q[0] = torch.from_numpy(src).to(q.device)
+    idx = faiss.IndexFlatL2(768)
+    idx.reserve(xb.shape[0])
+    st = torch.cuda.current_stream().cuda_stream
+    for blk in blocks:
+        idx.add_device(blk.data_ptr(), blk.shape[0], st)
+    del blocks
+    import ctypes as C
+    tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    _lib.check(_lib.load().knn_plan(idx.handle, NQ, K, C.byref(tr), C.byref(tq), C.byref(sp),
+                                    C.byref(wg)), "knn_plan")
+    assert (tr.value, tq.value, sp.value) == (256, 256, 64)      # the split layout the dups assume
+    D = torch.empty((NQ, K), dtype=torch.float32, device="cuda")
+    I = torch.empty((NQ, K), dtype=torch.int64, device="cuda")
+    idx.search_device(q.data_ptr(), NQ, K, D.data_ptr(), I.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert _lib.load().knn_last_path(idx.handle) == 2
+    stats = idx.certificate_stats()
+    print(f"cfg2: {stats}")
+    assert stats["candidate_queries"] == NQ and 0.0 <= stats["max_err_over_bound"] < 1.0
+    assert stats["exact_reruns"] >= 1                            # query 0, at least
+    Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
+    np.testing.assert_array_equal(Ih[0], _DUP_ROWS[:K])
+    assert (Dh[0] == 0.0).all()
+    xq = q.cpu().numpy()
+    sel = np.linspace(0, NQ - 1, NCHECK).astype(int)
+    check_knn(Dh[sel], Ih[sel], xb, xq[sel], K, "l2", min_exact_frac=0.5,
+              oracle=search_exact(xb, xq[sel], K + 1, "l2"))
+    Dc, Ic = c_oracle.flat_search(xb, xq[sel[:8]], K + 1, "l2")
+    check_knn(Dh[sel[:8]], Ih[sel[:8]], xb, xq[sel[:8]], K, "l2", min_exact_frac=0.5, oracle=(Dc, Ic))
+
+
+# --------------------------------------------------------------------------------------------
+# cfg4's whole answer (VERDICT r02 item 1): 10M x 1968 in one index over 8 row shards
+# --------------------------------------------------------------------------------------------
+def _device_oracle(torch, cfg_id, nrows, qs, k, need):
+    """float64 exact top-(k) of the queries qs (device tensor) over rows [0, nrows) of bench
+    config cfg_id, regenerated block by block on the device (bench.gen_rows: the same rows the
+    index holds), keeping the row vectors of the running top-k and of every label in `need`.
+    Returns (D float64, I int64, {label: float32 row})."""
+    import bench
+    cfg = dict(bench.CONFIGS[cfg_id])
+    dev = qs.device
+    centres = bench.make_centres(torch, cfg, dev, cfg_id)
+    qd = qs.double()
+    qn = (qd * qd).sum(1, keepdim=True)
+    nq, d = qs.shape
+    bd = torch.full((nq, k), float("inf"), dtype=torch.float64, device=dev)
+    bi = torch.full((nq, k), -1, dtype=torch.int64, device=dev)
+    bv = torch.zeros((nq, k, d), dtype=torch.float32, device=dev)
+    need_t = torch.tensor(sorted(need), dtype=torch.int64, device=dev)
+    rows, pos = {}, 0
+    for blk in bench.gen_rows(torch, cfg, centres, 0, nrows, dev, cfg_id):
+        n = blk.shape[0]
+        xd = blk.double()
+        dd = (qn + (xd * xd).sum(1)[None, :] - 2.0 * (qd @ xd.T)).clamp_min_(0.0)
+        v, i = torch.topk(dd, min(k, n), dim=1, largest=False)
+        cd = torch.cat([bd, v], 1)
+        ci = torch.cat([bi, i + pos], 1)
+        cv = torch.cat([bv, blk[i]], 1)
+        # (key, label) order: a stable sort by label, then a stable sort by key
+        o1 = torch.argsort(torch.where(ci < 0, torch.iinfo(torch.int64).max, ci), dim=1, stable=True)
+        o2 = torch.argsort(torch.gather(cd, 1, o1), dim=1, stable=True)
+        order = torch.gather(o1, 1, o2)[:, :k]
+        bd, bi = torch.gather(cd, 1, order), torch.gather(ci, 1, order)
+        bv = torch.gather(cv, 1, order[:, :, None].expand(-1, -1, d))
+        hit = need_t[(need_t >= pos) & (need_t < pos + n)]
+        for lab, r in zip(hit.tolist(), blk[hit - pos].cpu().numpy()):
+            rows[lab] = r
+        pos += n
+    for qi in range(nq):
+        for j in range(k):
+            rows[int(bi[qi, j])] = bv[qi, j].cpu().numpy()
+    return bd.cpu().numpy(), bi.cpu().numpy(), rows
+
+
+def test_cfg4_whole_10m_corpus_eight_shards(faiss):
+    """cfg4's whole corpus: 10M x 1968 concat rows in ONE IndexFlatL2 over 8 row shards
+    (knn_create_multi, devices [0]*8: fp32 + bf16 copies of every shard, ~120 GB of the 288 GB),
+    1024 queries on AUTO, the shards' top-k merged by knn_merge_kernel.  16 sampled queries
+    against a float64 scan of the same 10M rows regenerated on the device.  (One GPU here: the
+    shards share device 0, so the cross-device peer copies of knn_multi.cpp do not run.)"""
+    import torch
+    import bench
+    from oracle.flat_knn import fp32_error_bound  # noqa: F401  (check_knn's bound)
+    cfg = dict(bench.CONFIGS[4])
+    n, d = cfg["rows"], sum(cfg["parts"])
+    dev = torch.device("cuda", 0)
+    centres = bench.make_centres(torch, cfg, dev, 4)
+    idx = faiss.IndexFlatL2(d, devices=[0] * 8)
+    assert idx.num_shards == 8
+    idx.reserve(n)
+    st = torch.cuda.current_stream().cuda_stream
+    for blk in bench.gen_rows(torch, cfg, centres, 0, n, dev, 4):
+        idx.add_device(blk.data_ptr(), blk.shape[0], st)
+    assert idx.ntotal == n
+    q = bench.gen_queries(torch, cfg, centres, NQ, dev, 4)
+    D = torch.empty((NQ, K), dtype=torch.float32, device="cuda")
+    I = torch.empty((NQ, K), dtype=torch.int64, device="cuda")
+    idx.search_device(q.data_ptr(), NQ, K, D.data_ptr(), I.data_ptr(), st)
+    torch.cuda.synchronize()
+    stats = idx.certificate_stats()
+    print(f"cfg4 10M: {stats}")
+    assert stats["candidate_queries"] == NQ and stats["max_err_over_bound"] < 1.0
+    sel = np.linspace(0, NQ - 1, 16).astype(int)
+    Dh, Ih = D.cpu().numpy()[sel], I.cpu().numpy()[sel]
+    assert (Ih >= 0).all() and (Ih < n).all()
+    Dg, Ig, rows = _device_oracle(torch, 4, n, q[sel], K + 1, set(Ih.ravel().tolist()))
+    labels = np.array(sorted(rows))
+    xb = np.stack([rows[int(l)] for l in labels])
+    remap = lambda a: np.searchsorted(labels, a)                 # noqa: E731
+    check_knn(Dh, remap(Ih), xb, q.cpu().numpy()[sel], K, "l2", min_exact_frac=0.5,
+              oracle=(Dg, remap(Ig)))
+    hits = sum(len(set(a.tolist()) & set(b[:K].tolist())) for a, b in zip(Ih, Ig))
+    assert hits / (K * len(sel)) == 1.0, hits                    # recall@10 on the sample
+    del idx
+    torch.cuda.synchronize()

@@ -104,3 +104,21 @@ def test_large_k_multi_device_index(faiss, k):
     idx.add(xb)
     D, I = idx.search(xq, k)
     check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.0)
+
+
+@pytest.mark.parametrize("n,d,nq,k", [(30000, 64, 100, 100), (130000, 64, 3, 1024),
+                                      (20000, 64, 2100, 40), (60000, 200, 40, 300)])
+def test_large_k_several_rounds(faiss, n, d, nq, k):
+    """Large k over SEVERAL GEMM rounds: the unsorted running list carried from round
+    to round (first = 0, nr = k), and with nq <= 64 S stripes carrying lists over rounds
+    (30000 x 100 / nq 100: one stripe, 4 rounds; 130000 x 1024 / nq 3: 8 stripes, 3 rounds;
+    2100 queries: two query blocks of the per-block workspace, 3 rounds; 60000 x 300 / nq 40:
+    27 stripes, 2 rounds)."""
+    xb = mixture(n, d, centres=40, seed=n + k + 7)
+    xq = mixture(nq, d, centres=40, seed=n + k + 8)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    D, I = idx.search(xq, k)
+    sel = np.arange(nq) if nq <= 16 else np.unique(np.concatenate(
+        [np.random.default_rng(1).choice(nq, 12, replace=False), [0, nq - 1, min(nq - 1, 2048)]]))
+    check_knn(D[sel], I[sel], xb, xq[sel], k, "l2", min_exact_frac=0.0)
