@@ -78,6 +78,10 @@ SIGNATURES = {
     "ingest_parse_f32": (_i64, [_vp, _i64, _vp, _i64]),
     "ingest_concat_rows": (_i64, [C.POINTER(_vp), _pi64, _i64, _i, _pi64, _vp, _vp]),
     "ingest_concat_packed": (_i64, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp]),
+    "ingest_scan_open": (_i, [C.c_char_p, C.c_char_p, _i, _pi64, C.POINTER(_vp)]),
+    "ingest_scan_next": (_i64, [_vp, _i64, _vp, _vp, _vp]),
+    "ingest_scan_close": (_i, [_vp]),
+    "ingest_scan_error": (C.c_char_p, []),
 }
 
 

@@ -13,8 +13,13 @@
 // Every byte is checked; anything else (torch tensors, other dtypes, big-endian) is reported as
 // INGEST_NOT_FAST so the caller falls back to pickle.loads, as the reference does.
 
+#include <dlfcn.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
+
+#include <mutex>
+#include <string>
 
 #include "../../include/imgrec_ingest.h"
 
@@ -183,6 +188,165 @@ int64_t ingest_concat_packed(const uint8_t* buf, const int64_t* offsets, const i
         if (st == 0) ++good;
     }
     return good;
+}
+
+}  // extern "C"
+
+// -----------------------------------------------------------------------------------------------
+// Native scan of the builder's SELECT (include/imgrec_ingest.h ingest_scan_*): the system SQLite
+// library (the one Python's sqlite3 module links, so the same query plan and row order) is opened
+// with dlopen and driven from C: sqlite3_step per row, the BLOB columns parsed in place
+// (sqlite3_column_blob, no copy) and written into the caller's float32 batch.
+// -----------------------------------------------------------------------------------------------
+namespace {
+
+struct Sqlite {
+    void* h = nullptr;
+    int (*open_v2)(const char*, void**, int, const char*);
+    int (*prepare_v2)(void*, const char*, int, void**, const char**);
+    int (*step)(void*);
+    int64_t (*column_int64)(void*, int);
+    const void* (*column_blob)(void*, int);
+    int (*column_bytes)(void*, int);
+    int (*column_type)(void*, int);
+    int (*finalize)(void*);
+    int (*close)(void*);
+    const char* (*errmsg)(void*);
+    bool ok = false;
+};
+
+Sqlite* sqlite_lib() {
+    static Sqlite s;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (const char* name : {"libsqlite3.so.0", "libsqlite3.so"}) {
+            s.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (s.h) break;
+        }
+        if (!s.h) return;
+#define IMGREC_SYM(field, sym) s.field = reinterpret_cast<decltype(s.field)>(dlsym(s.h, sym))
+        IMGREC_SYM(open_v2, "sqlite3_open_v2");
+        IMGREC_SYM(prepare_v2, "sqlite3_prepare_v2");
+        IMGREC_SYM(step, "sqlite3_step");
+        IMGREC_SYM(column_int64, "sqlite3_column_int64");
+        IMGREC_SYM(column_blob, "sqlite3_column_blob");
+        IMGREC_SYM(column_bytes, "sqlite3_column_bytes");
+        IMGREC_SYM(column_type, "sqlite3_column_type");
+        IMGREC_SYM(finalize, "sqlite3_finalize");
+        IMGREC_SYM(close, "sqlite3_close");
+        IMGREC_SYM(errmsg, "sqlite3_errmsg");
+#undef IMGREC_SYM
+        s.ok = s.open_v2 && s.prepare_v2 && s.step && s.column_int64 && s.column_blob &&
+               s.column_bytes && s.column_type && s.finalize && s.close && s.errmsg;
+    });
+    return s.ok ? &s : nullptr;
+}
+
+thread_local std::string g_scan_err;
+
+constexpr int kSqliteOpenReadonly = 0x1, kSqliteRow = 100, kSqliteDone = 101, kSqliteNull = 5;
+
+}  // namespace
+
+struct ingest_scan {
+    void* db = nullptr;
+    void* stmt = nullptr;
+    int nparts = 0;
+    int64_t dim = 0;
+    int64_t part_dims[64] = {};
+    bool done = false;
+};
+
+extern "C" {
+
+const char* ingest_scan_error(void) { return g_scan_err.c_str(); }
+
+int ingest_scan_open(const char* db_path, const char* sql, int nparts, const int64_t* part_dims,
+                     ingest_scan_t** out) {
+    if (!out || !db_path || !sql || nparts < 1 || nparts > 64 || !part_dims) {
+        g_scan_err = "bad arguments";
+        return -1;
+    }
+    *out = nullptr;
+    Sqlite* L = sqlite_lib();
+    if (!L) {
+        g_scan_err = "libsqlite3.so.0 not found or incomplete";
+        return -5;
+    }
+    ingest_scan* s = new ingest_scan();
+    s->nparts = nparts;
+    for (int j = 0; j < nparts; ++j) {
+        s->part_dims[j] = part_dims[j];
+        s->dim += part_dims[j];
+    }
+    if (L->open_v2(db_path, &s->db, kSqliteOpenReadonly, nullptr) != 0) {
+        g_scan_err = std::string("sqlite3_open_v2: ") + (s->db ? L->errmsg(s->db) : "failed");
+        if (s->db) L->close(s->db);
+        delete s;
+        return -4;
+    }
+    if (L->prepare_v2(s->db, sql, -1, &s->stmt, nullptr) != 0 || !s->stmt) {
+        g_scan_err = std::string("sqlite3_prepare_v2: ") + L->errmsg(s->db);
+        L->close(s->db);
+        delete s;
+        return -4;
+    }
+    *out = s;
+    return 0;
+}
+
+int64_t ingest_scan_next(ingest_scan_t* s, int64_t cap, int64_t* ids, float* out, int8_t* status) {
+    if (!s || cap <= 0 || !ids || !out || !status) {
+        g_scan_err = "bad arguments";
+        return -1;
+    }
+    Sqlite* L = sqlite_lib();
+    int64_t n = 0;
+    while (n < cap && !s->done) {
+        const int rc = L->step(s->stmt);
+        if (rc == kSqliteDone) {
+            s->done = true;
+            break;
+        }
+        if (rc != kSqliteRow) {
+            g_scan_err = std::string("sqlite3_step: ") + L->errmsg(s->db);
+            return -4;
+        }
+        ids[n] = L->column_int64(s->stmt, 0);
+        float* o = out + n * s->dim;
+        int8_t st = 0;
+        for (int j = 0; j < s->nparts && st == 0; ++j) {
+            const uint8_t* pl;
+            int64_t nb, ne;
+            const int col = j + 1;
+            const uint8_t* b = L->column_type(s->stmt, col) == kSqliteNull
+                                   ? nullptr
+                                   : static_cast<const uint8_t*>(L->column_blob(s->stmt, col));
+            const int64_t len = b ? L->column_bytes(s->stmt, col) : 0;
+            if (!b || !parse(b, len, &pl, &nb, &ne)) {
+                st = 1;
+            } else if (ne != s->part_dims[j]) {
+                st = 2;
+            } else {
+                memcpy(o, pl, (size_t)nb);
+                o += ne;
+            }
+        }
+        status[n] = st;
+        ++n;
+    }
+    return n;
+}
+
+int ingest_scan_close(ingest_scan_t* s) {
+    if (!s) return 0;
+    Sqlite* L = sqlite_lib();
+    if (L) {
+        if (s->stmt) L->finalize(s->stmt);
+        if (s->db) L->close(s->db);
+    }
+    delete s;
+    return 0;
 }
 
 }  // extern "C"

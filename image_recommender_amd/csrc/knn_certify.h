@@ -1,0 +1,270 @@
+// knn_certify.h — device code of the candidate paths' certificate shared by the rerank kernel
+// (knn_refine.hip) and the certificate tail kernel (knn_kernels.hip): the error bounds of one
+// query, the exact fp32 rerank dot products, the second chance over the raw per-split lists, and
+// the cross-workgroup hand-off primitives the tail kernel's device-planned exact re-run uses.
+// Device code only; included by .hip translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "knn_kernels.h"
+#include "wave_ops.h"
+
+namespace imgrec {
+
+template <typename I>
+__device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
+    return d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
+
+// Error bounds of one query's certificate (DESIGN.md "bf16 path" / "Split path").
+struct QueryBounds {
+    float qn, xm, nn, e_ip, c_fp, c_trunc;
+    int metric;
+    static constexpr float u = 1.0f / 8388608.f;   // 2^-23
+    __device__ __forceinline__ QueryBounds(const RerankArgs& a, int64_t q) {
+        metric = a.metric;
+        qn = a.qnorm[q];
+        xm = *a.xn_max;
+        c_fp = a.c_fp;
+        c_trunc = a.c_trunc;
+        nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
+        // |approximate q.x - q.x| for every row:
+        //   split: c_split |q| max|x|
+        //   bf16:  |q.(x - xh) + (q - qh).xh| + accumulation <= |q| R + dq (X + R) + c_acc |qh| |xh|
+        //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max
+        //          |x|, |qh| <= |q| + dq, |xh| <= X + R), inflated for the bound's fp32 evaluation
+        if (a.mode == kModeBF16) {
+            const float sq = sqrtf(qn), X = sqrtf(xm), R = *a.xr_max, dq = a.q_resid[q];
+            e_ip = (sq * R + dq * (X + R) + a.c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
+        } else {
+            e_ip = a.c_split * nn;
+        }
+    }
+    // |approx key - exact key| bound at key v
+    __device__ __forceinline__ float bound_a(float v) const {
+        return metric == 1 ? 2.f * e_ip + 2.f * u * (qn + xm + fabsf(v)) : e_ip;
+    }
+    // |fp32 rerank key - exact key| bound
+    __device__ __forceinline__ float bound_f(float v) const {
+        return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
+    }
+    // candidates with approximate key above this cannot reach the top k (the k best by
+    // approximate key have exact keys <= a_k + E_a)
+    // (a candidate key may sit up to c_trunc |a| below the approximate key it stands for: a
+    // lower bound everywhere it bounds rows from below; added where it bounds from above)
+    __device__ __forceinline__ float prefix_limit(float a_k) const {
+        return a_k + 2.02f * (bound_a(a_k) + bound_f(a_k) + trunc(a_k));
+    }
+    __device__ __forceinline__ float trunc(float a) const { return c_trunc * fabsf(a); }
+};
+
+// Exact fp32 dot products of one query with kRerankRows rows, one wave, lane-strided float4
+// chunks (x y z w FMAs) then a butterfly: a row's key has the same bits in every pass.
+// IT > 0: the query's chunks are in registers (qr); IT = 0: streamed with the rows.
+template <int IT>
+__device__ __forceinline__ void rerank_dots(const float4* __restrict__ q4, const float4 (&qr)[IT > 0 ? IT : 1],
+                                            int n4, int lane, const float4* const (&r4)[kRerankRows],
+                                            float (&acc)[kRerankRows]) {
+#pragma unroll
+    for (int v = 0; v < kRerankRows; ++v) acc[v] = 0.f;
+    if constexpr (IT > 0) {
+        float4 b[kRerankRows][IT];
+#pragma unroll
+        for (int v = 0; v < kRerankRows; ++v)
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int i = lane + 64 * it;
+                b[v][it] = i < n4 ? r4[v][i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                acc[v] = fmaf(qr[it].x, b[v][it].x, acc[v]);
+                acc[v] = fmaf(qr[it].y, b[v][it].y, acc[v]);
+                acc[v] = fmaf(qr[it].z, b[v][it].z, acc[v]);
+                acc[v] = fmaf(qr[it].w, b[v][it].w, acc[v]);
+            }
+    } else {
+#pragma unroll 4
+        for (int i = lane; i < n4; i += 64) {
+            const float4 qa = q4[i];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                const float4 bb = r4[v][i];
+                acc[v] = fmaf(qa.x, bb.x, acc[v]);
+                acc[v] = fmaf(qa.y, bb.y, acc[v]);
+                acc[v] = fmaf(qa.z, bb.z, acc[v]);
+                acc[v] = fmaf(qa.w, bb.w, acc[v]);
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < kRerankRows; ++v)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
+}
+
+__device__ __forceinline__ float rerank_key(float ip, float qn, float xnr, int metric) {
+    if (metric == 1) {
+        const float kv = fmaf(-2.f, ip, qn + xnr);
+        return kv < 0.f ? 0.f : kv;
+    }
+    return -ip;
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Second chance for one query the rerank could not certify (item `item` of chance_list): every
+// entry of the candidate pass's per-split lists with approximate key <= the prefix limit (those
+// above it cannot reach the top k) is reranked, and the certificate is re-run against the list
+// floor alone — the smallest last key of a full list, below which no row outside all lists can
+// be.  NW waves per workgroup.  A query it cannot settle goes to the exact re-run list
+// (stats[0]).
+struct SecondChanceLDS {
+    float w_key[kWideCap], w_apx[kWideCap];
+    int64_t w_lab[kWideCap];
+    float o_key[64];
+    int64_t o_lab[64];
+    int w_n;
+    unsigned w_tau;
+    float s_sk;
+};
+
+template <int NW>
+__device__ __forceinline__ void second_chance_item(const RerankArgs& a, int item,
+                                                   SecondChanceLDS& L) {
+    constexpr int NT = NW * 64;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc;
+    const int n4 = dp / 4;
+    const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
+    {
+        const int64_t q = a.chance_list[item];
+        const QueryBounds B(a, q);
+        // the same prefix limit as the first pass, from the merged candidates' k-th key
+        const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
+        const float thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
+        if (t == 0) {
+            L.w_n = 0;
+            L.w_tau = key_bits_ordered(INFINITY);
+            L.s_sk = -INFINITY;
+        }
+        if (t < 64) L.o_lab[t] = -1;
+        __syncthreads();
+        const float* rd = a.raw_d + q * a.raw_stride_q;
+        const int64_t* ri = a.raw_i + q * a.raw_stride_q;
+        const int km = a.raw_km, ne = a.raw_lists * km;
+        for (int l = t; l < a.raw_lists; l += NT) {
+            const int e = l * km + km - 1;
+            if (ri[e] >= 0) atomicMin(&L.w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
+        }
+        for (int e = t; e < ne; e += NT) {
+            const int64_t l = ri[e];
+            const float v = rd[e];
+            if (l >= 0 && v <= thr) {
+                const int s = atomicAdd(&L.w_n, 1);
+                if (s < kWideCap) { L.w_apx[s] = v; L.w_lab[s] = l; }
+            }
+        }
+        __syncthreads();
+        const int n = L.w_n;
+        bool ok = n <= kWideCap;
+        if (ok) {
+            const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
+            for (int c0 = wave; c0 < n; c0 += NW * kRerankRows) {
+                const float4* r4[kRerankRows];
+                float acc[kRerankRows];
+#pragma unroll
+                for (int v = 0; v < kRerankRows; ++v)
+                    r4[v] = reinterpret_cast<const float4*>(
+                        a.xb + (L.w_lab[min(c0 + NW * v, n - 1)] - a.id_offset) * dp);
+                rerank_dots<0>(q4, none, n4, lane, r4, acc);
+#pragma unroll
+                for (int v = 0; v < kRerankRows; ++v) {
+                    const int c = c0 + NW * v;
+                    if (lane == 0 && c < n)
+                        L.w_key[c] = rerank_key(acc[v], B.qn, a.xn[L.w_lab[c] - a.id_offset], metric);
+                }
+            }
+            __syncthreads();
+            // rank of every reranked entry by (key, label): labels are distinct (a row sits in
+            // one list)
+            for (int s = t; s < n; s += NT) {
+                const float kv = L.w_key[s];
+                const int64_t lb = L.w_lab[s];
+                int rank = 0;
+                for (int j = 0; j < n && rank < k; ++j)
+                    rank += ranks_before_r(L.w_key[j], L.w_lab[j], kv, lb) ? 1 : 0;
+                if (rank < k) {
+                    L.o_key[rank] = kv;
+                    L.o_lab[rank] = lb;
+                    if (rank == k - 1) L.s_sk = kv;
+                }
+                const float r = fabsf(L.w_apx[s] - kv) /
+                                (B.bound_a(L.w_apx[s]) + B.bound_f(kv) + B.trunc(L.w_apx[s]));
+                atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
+            }
+            __syncthreads();
+            // +inf floor: no list dropped a row, so every row was a candidate and W holds all
+            // that can matter
+            const float tauL = key_from_ordered(L.w_tau);
+            ok = tauL == INFINITY || (tauL - B.bound_a(tauL)) > (L.s_sk + B.bound_f(L.s_sk));
+        }
+        if (ok) {
+            if (t < k) {
+                const int64_t lb = L.o_lab[t];
+                a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
+                                        : ((metric == 1) ? L.o_key[t] : -L.o_key[t]);
+                a.I[q * k + t] = lb;
+            }
+        } else if (t == 0) {
+            a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
+        }
+        __syncthreads();                // LDS reused by the next item
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cross-workgroup hand-off (MI355X_MICROARCH.md "Valid forms"): producer = every storing wave's
+// vmcnt(0) wait, the workgroup barrier, then ONE lane's agent-scope release and counter add;
+// consumer = that lane's agent-scope acquire after the counter says so, vmcnt(0), then the
+// workgroup barrier before any plain load of the handed-off bytes.
+__device__ __forceinline__ void wg_release_stores() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// Lane 0: release, add 1 to *ctr (agent scope), return the value before the add.
+__device__ __forceinline__ int lane0_release_add(int* ctr) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void lane0_acquire() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Barrier over a grid whose workgroups are all resident (the caller sizes it so): *ctr counts
+// arrivals from 0 (zeroed before the launch); every workgroup's stores before it are visible to
+// every workgroup after it.  Polls with relaxed agent-scope loads (L2, not L1) and s_sleep.
+__device__ __forceinline__ void grid_barrier(int* ctr, int nwg) {
+    wg_release_stores();
+    if (threadIdx.x == 0) {
+        lane0_release_add(ctr);
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nwg)
+            __builtin_amdgcn_s_sleep(2);
+        lane0_acquire();
+    }
+    __syncthreads();
+}
+
+}  // namespace imgrec

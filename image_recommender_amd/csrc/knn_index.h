@@ -72,11 +72,11 @@ constexpr int64_t kQueryChunk = 8192;
 Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus);
 Plan make_split_plan(int64_t ntotal, int64_t nq, int kc, int cus);
 Plan make_b16_plan(int64_t ntotal, int64_t nq, int k, int cus, int dpb);
-// The exact re-run of uncertified queries: the (2,1) tile of make_plan (256 rows x 32 queries)
-// on a fixed grid, planned on device for whatever count the certificate leaves.
+// The exact re-run of uncertified queries (inside the certificate tail kernel): the (2,1) tile
+// of make_plan (256 rows x 32 queries), planned on device for whatever count the certificate
+// leaves.
 constexpr int kFallbackWR = 2;                 // lists per row split = 2 * kFallbackWR
 int fallback_km(int k);
-int fallback_grid(int cus, int64_t chunk_q);
 int split_kc(int k);
 float split_coef(int dp);
 float rerank_coef(int dp);
@@ -136,7 +136,7 @@ struct knn_index {
     float* fb_qn = nullptr; size_t fb_qn_cap = 0;
     float* fb_cd = nullptr; size_t fb_cd_cap = 0;
     int64_t* fb_ci = nullptr; size_t fb_ci_cap = 0;
-    int* fb_dyn = nullptr;
+    int* tail_ctl = nullptr; size_t tail_ctl_cap = 0;   // tail claim counters + block tickets
     // host-path staging
     float* hq = nullptr; size_t hq_cap = 0;
     float* hd = nullptr; size_t hd_cap = 0;

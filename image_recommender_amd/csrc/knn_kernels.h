@@ -31,11 +31,6 @@ struct TileArgs {
     int64_t* cand_i;            // nq x ncand labels
     int ncand;
     int ib = 0;                 // 256 x 256 bf16 kernel: > 0 = packed lists with ib index bits
-    // device-planned launch (the exact re-run of uncertified queries): when set, the kernel reads
-    // {nq, nqb, nsplit, ncand} from dyn[0..3] and the grid has `grid` workgroups, those beyond
-    // nqb * nsplit exiting at once
-    const int* dyn = nullptr;
-    int grid = 0;
 };
 
 // One rerank + certificate launch over merged candidate-pass candidates (knn_refine.hip).
@@ -75,6 +70,30 @@ struct RerankArgs {
     const int64_t* raw_i = nullptr;
     int raw_lists = 0, raw_km = 0;
     int64_t raw_stride_q = 0;
+    int* tail_ctl = nullptr;    // the certificate tail's grid-barrier counters (zeroed by the rerank)
+};
+
+// The certificate tail of a candidate chunk (knn_kernels.hip cert_tail_kernel), ONE launch after
+// the rerank: the second chance over the raw per-split lists, the stats fold, and the exact fp32
+// re-run of the queries neither certificate settled (query gather, the (2,1) exact tile over a
+// device-planned set of (query block, row split) items, and the per-query-block merge scattered
+// into D / I).  With no query queued (the common case) it folds the stats and exits.
+struct TailArgs {
+    RerankArgs r;               // the rerank's arguments (second chance; stats, lists, D, I)
+    int parity, first;          // this chunk's stats parity; first chunk of the search
+    int* stat;                  // 12 ints: two chunk parities + the search accumulators
+    const float* qpad;          // the chunk's padded fp32 queries and norms (re-run input)
+    const float* qnorm;
+    int dp, nrows, ntiles, metric;
+    const float* xb;            // fp32 corpus + norms
+    const float* xn;
+    int64_t id_offset;
+    float* fq;                  // gathered re-run queries (cap_rows x dp) and norms
+    float* fqn;
+    float* fcd;                 // re-run candidate lists
+    int64_t* fci;
+    int* ticket;                // per query block: row splits done (zeroed in the kernel)
+    int km, lists_km;           // list length, lists per row split x km
 };
 
 constexpr int kTileRowsMax = 256;   // corpus capacity is rounded to this many rows
@@ -160,18 +179,9 @@ hipError_t launch_map_labels(int64_t* I, int64_t n, const int64_t* lmap, int64_t
 hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32_t* dst,
                              hipStream_t st);
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st);
-// Plan + query gather of the device-side exact re-run (knn_refine.hip fallback_prep_kernel):
-// stat = 3 x 4 ints (two chunk parities + the search accumulators), list = the uncertified
-// queries; fq/fqn hold cap_rows rows (cap_rows >= the chunk's queries rounded up to 32);
-// lists_km = candidate lists per row split x their length.
-hipError_t launch_fallback_prep(int* stat, int parity, int first, const int* list, const float* qpad,
-                                const float* qnorm, int dp, int grid_wgs, int ntiles, int lists_km,
-                                int64_t cap_rows, float* fq, float* fqn, int* dyn, hipStream_t st);
-// Merge of a device-planned launch's lists (nq, nlists, stride from dyn, grid cap_q queries) with
-// the results scattered to rows out_rows[q] of D, I.
-hipError_t launch_merge_dyn(const float* cd, const int64_t* ci, const int* dyn, int lists_per_split,
-                            int kin, int64_t cap_q, int k, int metric, const int* out_rows,
-                            float* D, int64_t* I, hipStream_t st);
+// The certificate tail (TailArgs) on `grid` resident workgroups of the (2,1) exact tile.
+hipError_t launch_cert_tail(const TailArgs& a, int grid, hipStream_t st);
+constexpr int kTailWGPerCU = 1;     // tail grid = kTailWGPerCU x CUs (work is claimed, never awaited)
 hipError_t launch_gather_rows(const float* src, const float* src_norm, int dp, const int* list,
                               int64_t n, int64_t n_pad, float* dst, float* dst_norm, hipStream_t st);
 hipError_t launch_scatter_results(const float* sd, const int64_t* si, const int* list, int64_t n,

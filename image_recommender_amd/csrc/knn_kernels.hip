@@ -29,6 +29,7 @@
 #include <float.h>
 #include <math.h>
 
+#include "knn_certify.h"
 #include "knn_kernels.h"
 #include "wave_ops.h"
 
@@ -218,36 +219,21 @@ __device__ __forceinline__ void list_insert_mono(float (&kd)[K], int (&ki)[K], f
 
 // 4-wave workgroups run two per CU (two waves per SIMD): hold them to 256 VGPR+AGPR per lane.
 #define IMGREC_MIN_WAVES(nw) ((nw) == 4 ? 2 : 1)
+// The work of one (query block, row split) item `wgid` (query block wgid % nqb, split
+// wgid / nqb), in the LDS array smem (G::LDS_FLOATS floats).  The kernel below runs one item per
+// workgroup; the certificate tail kernel loops over the items of a device-planned exact re-run.
 template <int WR, int WQ, int KM, int NS, int BK, int MODE, int WB>
-__global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
-knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
-                     int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
-                     int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
-                     float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand,
-                     const int* __restrict__ dyn) {
+__device__ __forceinline__ void tile_topk_item(
+        const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows, int dp,
+        const float* __restrict__ qp, const float* __restrict__ qnorm, int nq, int metric,
+        int ntiles, int nsplit, int nqb, int64_t id_offset, float* __restrict__ cand_d,
+        int64_t* __restrict__ cand_i, int ncand, int wgid, float* __restrict__ smem) {
     using G = TileGeom<WR, WQ, NS, BK, WB>;
     constexpr int RW = G::RW;
     constexpr int NW = G::NW, BM = G::BM, BQ = G::BQ, SA = G::SA, STAGE = G::STAGE;
     constexpr int PA = G::PA, LPW = G::LPW, CPR = G::CPR, RPP = G::RPP, RPB = G::RPB, PR = G::PR;
     constexpr int KH = BK / 2;          // MFMA sub-steps per stage (each covers depth 2)
-
-    __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
     float* const norm_base = smem + NS * STAGE;
-
-    // XCD-aware, bijective block -> (query block, row split) map: blocks b and b+8 share an XCD;
-    // consecutive remapped ids (same XCD) share a row split, so the corpus stages they stream are
-    // served from that XCD's L2 for all query blocks.
-    const int nwg = gridDim.x, wg = blockIdx.x;
-    const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
-    if (dyn) {                              // device-planned launch (exact re-run)
-        nq = dyn[0];
-        nqb = dyn[1];
-        nsplit = dyn[2];
-        ncand = dyn[3];
-        if (nq <= 0) return;
-    }
-    if (wgid >= nqb * nsplit) return;       // only a device-planned grid has spare workgroups
     const int qb = wgid % nqb;
     const int split = wgid / nqb;
     // this split's tiles, in increasing order: tile(j) for j in [0, t1).  Round-robin (split s
@@ -483,6 +469,26 @@ knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xno
     }
 }
 
+template <int WR, int WQ, int KM, int NS, int BK, int MODE, int WB>
+__global__ void __launch_bounds__(WR * WQ * 64, IMGREC_MIN_WAVES(WR * WQ))
+knn_tile_topk_kernel(const float* __restrict__ xb, const float* __restrict__ xnorm, int nrows,
+                     int dp, const float* __restrict__ qp, const float* __restrict__ qnorm, int nq,
+                     int metric, int ntiles, int nsplit, int nqb, int64_t id_offset,
+                     float* __restrict__ cand_d, int64_t* __restrict__ cand_i, int ncand) {
+    using G = TileGeom<WR, WQ, NS, BK, WB>;
+    __shared__ __attribute__((aligned(16))) float smem[G::LDS_FLOATS];
+    // XCD-aware, bijective block -> (query block, row split) map: blocks b and b+8 share an XCD;
+    // consecutive remapped ids (same XCD) share a row split, so the corpus stages they stream are
+    // served from that XCD's L2 for all query blocks.
+    const int nwg = gridDim.x, wg = blockIdx.x;
+    const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
+    if (wgid >= nqb * nsplit) return;
+    tile_topk_item<WR, WQ, KM, NS, BK, MODE, WB>(xb, xnorm, nrows, dp, qp, qnorm, nq, metric,
+                                                 ntiles, nsplit, nqb, id_offset, cand_d, cand_i,
+                                                 ncand, wgid, smem);
+}
+
 // ---------------------------------------------------------------------------------------------
 // knn_merge: WPQ waves per query.  The input is nlists candidate lists per query, each sorted
 // best-first (the fused kernel's per-lane lists, or gathered per-shard results); list l of query q
@@ -616,31 +622,208 @@ __device__ __forceinline__ void merge_block(const float* __restrict__ cd, const 
     }
 }
 
-// dyn (device-planned lists of the exact re-run): nq, lists and stride come from dyn, and the
-// grid (fixed, small: a near-empty launch when nothing is re-run) loops over the queries.
 template <int KM, int WPQ>
 __global__ void __launch_bounds__(256)
 knn_merge_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
                  int nlists, int kin, int64_t stride_q, int64_t stride_l, int64_t stride_li, int k,
                  int metric, int negate_in, float* __restrict__ D, int64_t* __restrict__ I,
-                 float* __restrict__ floor_out, const int* __restrict__ dyn, int dyn_lists,
-                 const int* __restrict__ out_rows) {
+                 float* __restrict__ floor_out) {
     __shared__ float sd[4][KM];
     __shared__ int64_t si[4][KM];
-    if (!dyn) {
-        merge_block<KM, WPQ>(cd, ci, blockIdx.x, nq, nlists, kin, stride_q, stride_l, stride_li, k,
-                             metric, negate_in, D, I, floor_out, out_rows, sd, si);
+    merge_block<KM, WPQ>(cd, ci, blockIdx.x, nq, nlists, kin, stride_q, stride_l, stride_li, k,
+                         metric, negate_in, D, I, floor_out, nullptr, sd, si);
+}
+
+// One wave merges query q's nlists sorted lists of kin entries (list l at q * stride_q + l * kin,
+// label -1 = empty) into output row orow of D / I (faiss convention).  The certificate tail's
+// exact re-run: a query block's lists are merged by the workgroup that finished its last split.
+template <int KM>
+__device__ __forceinline__ void merge_query_wave(const float* __restrict__ cd,
+                                                 const int64_t* __restrict__ ci, int64_t q,
+                                                 int nlists, int kin, int64_t stride_q, int k,
+                                                 int metric, float* __restrict__ D,
+                                                 int64_t* __restrict__ I, int64_t orow) {
+    const int lane = threadIdx.x & 63;
+    float kd[KM];
+    int64_t ki[KM];
+#pragma unroll
+    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+    for (int l = lane; l < nlists; l += 64) {
+        const float* lp = cd + q * stride_q + (int64_t)l * kin;
+        const int64_t* ip = ci + q * stride_q + (int64_t)l * kin;
+        for (int p = 0; p < kin; ++p) {
+            const int64_t id = ip[p];
+            const float d = lp[p];
+            if (id < 0 || !ranks_before(d, id, kd[KM - 1], ki[KM - 1])) break;   // sorted list
+            list_insert<KM, int64_t>(kd, ki, d, id);
+        }
+    }
+    wave_select<KM>(kd, ki, k, lane, D + orow * k, I + orow * k, 1, metric);
+}
+
+// ---------------------------------------------------------------------------------------------
+// cert_tail_kernel<KM>: everything after the rerank of a candidate chunk in ONE launch (it was
+// four: second chance, re-run plan, exact tile, merge — each ~4.5 us even when empty, most of it
+// the kernel boundary and a dependent load of a device count).  Reads the chunk's counts, which
+// the rerank wrote: with nothing queued, workgroup 0 folds the stats and every workgroup exits.
+// Otherwise, with no workgroup ever waiting on one that has not yet claimed work (so the launch
+// cannot deadlock whatever else shares the GPU — the multi-device index runs shards concurrently
+// on one device):
+//   1. second-chance items are claimed from ctl[0], completions counted in ctl[1]; the workgroup
+//      that completes the last one (or takes ticket 0 when none was queued) is the planner;
+//   2. the planner folds the stats, gathers the uncertified queries (fail_list) into fq / fqn
+//      (zero rows up to a multiple of 32), zeroes the per-query-block tickets and publishes
+//      ctl[2] = 1; everyone else waits for it (the planner is running: it completed an item);
+//   3. exact (2,1)-tile items (query block, row split) are claimed from ctl[3]; the workgroup
+//      that finishes a query block's last split merges that block's lists into the rows
+//      fail_list[q] of D / I.
+// ctl[0..3] are zeroed by the rerank kernel (the launch before this one on the stream).
+// ---------------------------------------------------------------------------------------------
+constexpr int kTailWR = 2, kTailNS = 3, kTailBK = 16, kTailWB = 4, kTailWaves = kTailWR;
+
+template <int KM>
+__global__ void __launch_bounds__(kTailWaves * 64, 1)
+cert_tail_kernel(const TailArgs a) {
+    using G = TileGeom<kTailWR, 1, kTailNS, kTailBK, kTailWB>;
+    constexpr int kFloats = G::LDS_FLOATS > (int)(sizeof(SecondChanceLDS) / 4 + 1)
+                                ? G::LDS_FLOATS : (int)(sizeof(SecondChanceLDS) / 4 + 1);
+    __shared__ __attribute__((aligned(16))) float smem[kFloats];
+    __shared__ int s_val;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    int* const sp = a.stat + 4 * a.parity;
+    int* const ctl = a.r.tail_ctl;
+    const int n_chance = sp[3];                 // final: the rerank kernel has completed
+    if (n_chance == 0 && sp[0] == 0) {          // the common case: every query certified
+        if (blockIdx.x == 0 && t == 0) {
+            int* acc = a.stat + 8;
+            acc[0] = a.first ? 0 : acc[0];
+            acc[1] = a.first ? sp[1] : max(acc[1], sp[1]);   // ratio >= 0: bit order = float order
+            acc[2] = a.first ? sp[2] : acc[2] + sp[2];
+            int* other = a.stat + 4 * (a.parity ^ 1);
+            other[0] = 0; other[1] = 0; other[2] = 0; other[3] = 0;
+        }
         return;
     }
-    nq = dyn[0];
-    nlists = dyn[2] * dyn_lists;
-    stride_q = dyn[3];
-    constexpr int QPB = 4 / WPQ;
-    for (int64_t blk = blockIdx.x; blk * QPB < nq; blk += gridDim.x) {
-        merge_block<KM, WPQ>(cd, ci, blk, nq, nlists, kin, stride_q, stride_l, stride_li, k, metric,
-                             negate_in, D, I, floor_out, out_rows, sd, si);
-        __syncthreads();                          // sd / si reused by the next query
+    // ---- 1. second chance ----------------------------------------------------------------
+    bool planner = false;
+    if (n_chance > 0) {
+        for (;;) {
+            if (t == 0) s_val = __hip_atomic_fetch_add(ctl + 0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            const int item = s_val;
+            __syncthreads();
+            if (item >= n_chance) break;
+            second_chance_item<kTailWaves>(a.r, item, *reinterpret_cast<SecondChanceLDS*>(smem));
+            wg_release_stores();
+            if (t == 0) {
+                const int done = lane0_release_add(ctl + 1);
+                s_val = done == n_chance - 1;
+                if (s_val) lane0_acquire();
+            }
+            __syncthreads();
+            planner = planner || s_val != 0;
+            __syncthreads();
+        }
+    } else {
+        if (t == 0) s_val = __hip_atomic_fetch_add(ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+        __syncthreads();
+        planner = s_val != 0;
+        __syncthreads();
     }
+    // ---- 2. plan + query gather (one workgroup) ------------------------------------------
+    if (planner) {
+        const int count = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int nqb = (count + 31) / 32;
+        if (t == 0) {
+            int* acc = a.stat + 8;
+            acc[0] = a.first ? count : acc[0] + count;
+            acc[1] = a.first ? sp[1] : max(acc[1], sp[1]);
+            acc[2] = a.first ? sp[2] : acc[2] + sp[2];
+            int* other = a.stat + 4 * (a.parity ^ 1);
+            other[0] = 0; other[1] = 0; other[2] = 0; other[3] = 0;
+        }
+        for (int i = t; i < nqb; i += kTailWaves * 64) a.ticket[i] = 0;
+        for (int row = wave; row < nqb * 32; row += kTailWaves) {
+            float* o = a.fq + (int64_t)row * a.dp;
+            if (row >= count) {
+                for (int j = lane; j < a.dp; j += 64) o[j] = 0.f;
+                if (lane == 0) a.fqn[row] = 0.f;
+                continue;
+            }
+            const int src = a.r.fail_list[row];
+            const float* s = a.qpad + (int64_t)src * a.dp;
+            for (int j = lane; j < a.dp; j += 64) o[j] = s[j];
+            if (lane == 0) a.fqn[row] = a.qnorm[src];
+        }
+        wg_release_stores();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        if (t == 0) {
+            // the planner is running (it completed an item or took ticket 0); the bound only
+            // turns a broken invariant into a reported error (stats bit) instead of a hang
+            int spins = 0;
+            s_val = 0;
+            while (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1 << 26)) { s_val = 1; break; }
+            }
+            if (s_val) atomicOr(a.stat + 11, 1);
+            lane0_acquire();
+        }
+        __syncthreads();
+        if (s_val) return;
+    }
+    const int count = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (count == 0) return;
+    // ---- 3. exact re-run: (query block, row split) items, merged by each block's last split ----
+    const int nqb = (count + 31) / 32;
+    const int nsplit = max(1, min((int)gridDim.x / nqb, a.ntiles));
+    const int nitems = nqb * nsplit;
+    const int ncand = nsplit * a.lists_km;
+    for (;;) {
+        if (t == 0) s_val = __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int item = s_val;
+        __syncthreads();
+        if (item >= nitems) break;
+        tile_topk_item<kTailWR, 1, KM, kTailNS, kTailBK, kModeF32, kTailWB>(
+            a.xb, a.xn, a.nrows, a.dp, a.fq, a.fqn, count, a.metric, a.ntiles, nsplit, nqb,
+            a.id_offset, a.fcd, a.fci, ncand, item, smem);
+        const int qb = item % nqb;
+        wg_release_stores();
+        if (t == 0) {
+            const int done = lane0_release_add(a.ticket + qb);
+            s_val = done == nsplit - 1;
+            if (s_val) lane0_acquire();
+        }
+        __syncthreads();
+        if (s_val) {
+            for (int ql = qb * 32 + wave; ql < min(count, qb * 32 + 32); ql += kTailWaves)
+                merge_query_wave<KM>(a.fcd, a.fci, ql, ncand / KM, KM, ncand, a.r.k, a.metric,
+                                     a.r.D, a.r.I, a.r.fail_list[ql]);
+        }
+        __syncthreads();                        // s_val and the LDS ring reused by the next item
+    }
+}
+
+hipError_t launch_cert_tail(const TailArgs& a, int grid, hipStream_t st) {
+    if (grid <= 0 || !a.r.tail_ctl || !a.ticket || a.dp % kTailBK != 0) return hipErrorInvalidValue;
+    if (a.lists_km != 2 * kTailWR * a.km) return hipErrorInvalidValue;
+#define IMGREC_TAIL(KMV) hipLaunchKernelGGL((cert_tail_kernel<KMV>), dim3((unsigned)grid), \
+                                            dim3(kTailWaves * 64), 0, st, a)
+    switch (a.km) {
+        case 8: IMGREC_TAIL(8); break;
+        case 10: IMGREC_TAIL(10); break;
+        case 16: IMGREC_TAIL(16); break;
+        case 32: IMGREC_TAIL(32); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef IMGREC_TAIL
+    return hipGetLastError();
 }
 
 __global__ void fill_empty_kernel(float* __restrict__ D, int64_t* __restrict__ I, int64_t n,
@@ -663,11 +846,11 @@ hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_
 
 template <int WR, int WQ, int NS, int BK, int MODE = kModeF32, int WB = 4>
 static hipError_t launch_tile_km(int km, const TileArgs& a, hipStream_t st) {
-    const dim3 grid((unsigned)(a.dyn ? a.grid : a.nqb * a.nsplit)), block(WR * WQ * 64);
+    const dim3 grid((unsigned)(a.nqb * a.nsplit)), block(WR * WQ * 64);
 #define IMGREC_LAUNCH_TILE(KMV)                                                                   \
     hipLaunchKernelGGL((knn_tile_topk_kernel<WR, WQ, KMV, NS, BK, MODE, WB>), grid, block, 0, st, a.xb, \
                        a.xnorm, a.nrows, a.dp, a.qp, a.qnorm, a.nq, a.metric, a.ntiles, a.nsplit, \
-                       a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand, a.dyn)
+                       a.nqb, a.id_offset, a.cand_d, a.cand_i, a.ncand)
     switch (km) {
         case 8: IMGREC_LAUNCH_TILE(8); break;
         case 10: IMGREC_LAUNCH_TILE(10); break;
@@ -731,12 +914,10 @@ hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, 
     do {                                                                                            \
         if (wide)                                                                                   \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr,      \
-                               nullptr, 0, nullptr);                                              \
+                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr); \
         else                                                                                        \
             hipLaunchKernelGGL((knn_merge_kernel<KMV, 1>), grid, block, 0, st, cd, ci, nq, nlists, \
-                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr,      \
-                               nullptr, 0, nullptr);                                              \
+                               kin, stride_q, stride_l, stride_li, k, metric, negate_in, D, I, nullptr); \
     } while (0)
     if (k <= 8) IMGREC_LAUNCH_MERGE(8);
     else if (k <= 10) IMGREC_LAUNCH_MERGE(10);
@@ -923,27 +1104,7 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
     // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is
     // covered by the floor), the output takes kout rounds of the wave argmin
     hipLaunchKernelGGL((knn_merge_kernel<16, 1>), dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
-                       cd, ci, nq, nlists, kin, stride_q, stride_l, stride_l, kout, 1, 0, D, I, floor,
-                       nullptr, 0, nullptr);
-    return hipGetLastError();
-}
-
-hipError_t launch_merge_dyn(const float* cd, const int64_t* ci, const int* dyn, int lists_per_split,
-                            int kin, int64_t cap_q, int k, int metric, const int* out_rows,
-                            float* D, int64_t* I, hipStream_t st) {
-    if (cap_q <= 0) return hipSuccess;
-    // four waves per query (the plan can give one query block all the row splits); the grid loops
-    const dim3 grid((unsigned)std::min<int64_t>(cap_q, 256)), block(256);
-#define IMGREC_MERGE_DYN(KMV)                                                                      \
-    hipLaunchKernelGGL((knn_merge_kernel<KMV, 4>), grid, block, 0, st, cd, ci, cap_q, 0, kin,      \
-                       (int64_t)0, (int64_t)kin, (int64_t)kin, k, metric, 0, D, I, nullptr, dyn,   \
-                       lists_per_split, out_rows)
-    if (k <= 8) IMGREC_MERGE_DYN(8);
-    else if (k <= 10) IMGREC_MERGE_DYN(10);
-    else if (k <= 16) IMGREC_MERGE_DYN(16);
-    else if (k <= 32) IMGREC_MERGE_DYN(32);
-    else return hipErrorInvalidValue;
-#undef IMGREC_MERGE_DYN
+                       cd, ci, nq, nlists, kin, stride_q, stride_l, stride_l, kout, 1, 0, D, I, floor);
     return hipGetLastError();
 }
 

@@ -34,12 +34,6 @@ Plan make_plan(int64_t ntotal, int64_t nq, int k, int cus) {
 
 int fallback_km(int k) { return k <= 8 ? 8 : (k <= 10 ? 10 : (k <= 16 ? 16 : 32)); }
 
-// Three (2,1) workgroups per CU (make_plan's geometry for <= 32 queries), and never fewer than
-// one per 32-query block of a full chunk, so every block of the device plan gets a workgroup.
-int fallback_grid(int cus, int64_t chunk_q) {
-    return (int)std::max<int64_t>(3 * (int64_t)cus, (chunk_q + 31) / 32);
-}
-
 // Split-path geometry: one tile shape for every batch size ((1,4) workgroups, two per CU,
 // kSplitWB row blocks per wave).
 Plan make_split_plan(int64_t ntotal, int64_t nq, int kc, int cus) {

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "knn_certify.h"
 #include "knn_kernels.h"
 #include "wave_ops.h"
 
@@ -187,110 +188,6 @@ query_prep_b16_kernel(const float* __restrict__ src, int64_t n, int d, int dp, i
     }
 }
 
-template <typename I>
-__device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
-    return d1 < d2 || (d1 == d2 && i1 < i2);
-}
-
-constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
-
-// Error bounds of one query's certificate (DESIGN.md "bf16 path" / "Split path").
-struct QueryBounds {
-    float qn, xm, nn, e_ip, c_fp, c_trunc;
-    int metric;
-    static constexpr float u = 1.0f / 8388608.f;   // 2^-23
-    __device__ __forceinline__ QueryBounds(const RerankArgs& a, int64_t q) {
-        metric = a.metric;
-        qn = a.qnorm[q];
-        xm = *a.xn_max;
-        c_fp = a.c_fp;
-        c_trunc = a.c_trunc;
-        nn = sqrtf(qn) * sqrtf(xm) * (1.f + 1.0f / 1024.f) + 1e-30f;
-        // |approximate q.x - q.x| for every row:
-        //   split: c_split |q| max|x|
-        //   bf16:  |q.(x - xh) + (q - qh).xh| + accumulation <= |q| R + dq (X + R) + c_acc |qh| |xh|
-        //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max
-        //          |x|, |qh| <= |q| + dq, |xh| <= X + R), inflated for the bound's fp32 evaluation
-        if (a.mode == kModeBF16) {
-            const float sq = sqrtf(qn), X = sqrtf(xm), R = *a.xr_max, dq = a.q_resid[q];
-            e_ip = (sq * R + dq * (X + R) + a.c_split * (sq + dq) * (X + R)) * (1.f + 1.0f / 256.f) + 1e-30f;
-        } else {
-            e_ip = a.c_split * nn;
-        }
-    }
-    // |approx key - exact key| bound at key v
-    __device__ __forceinline__ float bound_a(float v) const {
-        return metric == 1 ? 2.f * e_ip + 2.f * u * (qn + xm + fabsf(v)) : e_ip;
-    }
-    // |fp32 rerank key - exact key| bound
-    __device__ __forceinline__ float bound_f(float v) const {
-        return metric == 1 ? 2.f * c_fp * nn + 2.f * u * (qn + xm + fabsf(v)) : c_fp * nn;
-    }
-    // candidates with approximate key above this cannot reach the top k (the k best by
-    // approximate key have exact keys <= a_k + E_a)
-    // (a candidate key may sit up to c_trunc |a| below the approximate key it stands for: a
-    // lower bound everywhere it bounds rows from below; added where it bounds from above)
-    __device__ __forceinline__ float prefix_limit(float a_k) const {
-        return a_k + 2.02f * (bound_a(a_k) + bound_f(a_k) + trunc(a_k));
-    }
-    __device__ __forceinline__ float trunc(float a) const { return c_trunc * fabsf(a); }
-};
-
-// Exact fp32 dot products of one query with kRerankRows rows, one wave, lane-strided float4
-// chunks (x y z w FMAs) then a butterfly: a row's key has the same bits in every pass.
-// IT > 0: the query's chunks are in registers (qr); IT = 0: streamed with the rows.
-template <int IT>
-__device__ __forceinline__ void rerank_dots(const float4* __restrict__ q4, const float4 (&qr)[IT > 0 ? IT : 1],
-                                            int n4, int lane, const float4* const (&r4)[kRerankRows],
-                                            float (&acc)[kRerankRows]) {
-#pragma unroll
-    for (int v = 0; v < kRerankRows; ++v) acc[v] = 0.f;
-    if constexpr (IT > 0) {
-        float4 b[kRerankRows][IT];
-#pragma unroll
-        for (int v = 0; v < kRerankRows; ++v)
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                const int i = lane + 64 * it;
-                b[v][it] = i < n4 ? r4[v][i] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-        for (int it = 0; it < IT; ++it)
-#pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
-                acc[v] = fmaf(qr[it].x, b[v][it].x, acc[v]);
-                acc[v] = fmaf(qr[it].y, b[v][it].y, acc[v]);
-                acc[v] = fmaf(qr[it].z, b[v][it].z, acc[v]);
-                acc[v] = fmaf(qr[it].w, b[v][it].w, acc[v]);
-            }
-    } else {
-#pragma unroll 4
-        for (int i = lane; i < n4; i += 64) {
-            const float4 qa = q4[i];
-#pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
-                const float4 bb = r4[v][i];
-                acc[v] = fmaf(qa.x, bb.x, acc[v]);
-                acc[v] = fmaf(qa.y, bb.y, acc[v]);
-                acc[v] = fmaf(qa.z, bb.z, acc[v]);
-                acc[v] = fmaf(qa.w, bb.w, acc[v]);
-            }
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < kRerankRows; ++v)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) acc[v] += __shfl_xor(acc[v], off, 64);
-}
-
-__device__ __forceinline__ float rerank_key(float ip, float qn, float xnr, int metric) {
-    if (metric == 1) {
-        const float kv = fmaf(-2.f, ip, qn + xnr);
-        return kv < 0.f ? 0.f : kv;
-    }
-    return -ip;
-}
-
 // One workgroup of kRerankWaves waves per query.  a.cd/a.ci: the merged approximate candidates,
 // nq x kc, ascending raw keys (L2 distance or -ip), empty = label -1.
 // IT > 0: the query row sits in registers (IT float4 per lane, dp <= 256 IT) and every wave loads
@@ -308,6 +205,8 @@ rerank_certify_kernel(const RerankArgs a) {
     const int64_t q = blockIdx.x;
     const int dp = a.dp, kc = a.kc, k = a.k, metric = a.metric;
     const int64_t id_offset = a.id_offset;
+    // the certificate tail kernel's grid-barrier counters start from zero (it runs next)
+    if (a.tail_ctl && blockIdx.x == 0 && threadIdx.x < 4) a.tail_ctl[threadIdx.x] = 0;
     const float* __restrict__ cd = a.cd;
     const int64_t* __restrict__ ci = a.ci;
     const int64_t lab = lane < kc ? ci[q * kc + lane] : (int64_t)-1;
@@ -432,156 +331,6 @@ rerank_certify_kernel(const RerankArgs a) {
     }
 }
 
-// Second chance for the queries the rerank could not certify (stats[3] of them in chance_list):
-// every entry of the candidate pass's per-split lists with approximate key <= the prefix limit
-// (those above it cannot reach the top k) is reranked, and the certificate is re-run against
-// the list floor alone — the smallest last key of a full list, below which no row outside all
-// lists can be.  A workgroup per listed query, the grid looping over the list (a fixed, small
-// grid: with nothing listed the launch is a few microseconds).  Queries it cannot settle go to
-// the exact re-run list (stats[0]).
-__global__ void __launch_bounds__(kRerankWaves * 64)
-second_chance_kernel(const RerankArgs a) {
-    __shared__ float w_key[kWideCap], w_apx[kWideCap];
-    __shared__ int64_t w_lab[kWideCap];
-    __shared__ float o_key[64];
-    __shared__ int64_t o_lab[64];
-    __shared__ int w_n;
-    __shared__ unsigned w_tau;
-    __shared__ float s_sk;
-    constexpr int NT = kRerankWaves * 64;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int count = a.stats[3];
-    const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc;
-    const int n4 = dp / 4;
-    const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
-    for (int item = blockIdx.x; item < count; item += gridDim.x) {
-        const int64_t q = a.chance_list[item];
-        const QueryBounds B(a, q);
-        // the same prefix limit as the first pass, from the merged candidates' k-th key
-        const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
-        const float thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
-        if (t == 0) {
-            w_n = 0;
-            w_tau = key_bits_ordered(INFINITY);
-            s_sk = -INFINITY;
-        }
-        if (t < 64) o_lab[t] = -1;
-        __syncthreads();
-        const float* rd = a.raw_d + q * a.raw_stride_q;
-        const int64_t* ri = a.raw_i + q * a.raw_stride_q;
-        const int km = a.raw_km, ne = a.raw_lists * km;
-        for (int l = t; l < a.raw_lists; l += NT) {
-            const int e = l * km + km - 1;
-            if (ri[e] >= 0) atomicMin(&w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
-        }
-        for (int e = t; e < ne; e += NT) {
-            const int64_t l = ri[e];
-            const float v = rd[e];
-            if (l >= 0 && v <= thr) {
-                const int s = atomicAdd(&w_n, 1);
-                if (s < kWideCap) { w_apx[s] = v; w_lab[s] = l; }
-            }
-        }
-        __syncthreads();
-        const int n = w_n;
-        bool ok = n <= kWideCap;
-        if (ok) {
-            const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
-            for (int c0 = wave; c0 < n; c0 += kRerankWaves * kRerankRows) {
-                const float4* r4[kRerankRows];
-                float acc[kRerankRows];
-#pragma unroll
-                for (int v = 0; v < kRerankRows; ++v)
-                    r4[v] = reinterpret_cast<const float4*>(
-                        a.xb + (w_lab[min(c0 + kRerankWaves * v, n - 1)] - a.id_offset) * dp);
-                rerank_dots<0>(q4, none, n4, lane, r4, acc);
-#pragma unroll
-                for (int v = 0; v < kRerankRows; ++v) {
-                    const int c = c0 + kRerankWaves * v;
-                    if (lane == 0 && c < n)
-                        w_key[c] = rerank_key(acc[v], B.qn, a.xn[w_lab[c] - a.id_offset], metric);
-                }
-            }
-            __syncthreads();
-            // rank of every reranked entry by (key, label): labels are distinct (a row sits in
-            // one list)
-            for (int s = t; s < n; s += NT) {
-                const float kv = w_key[s];
-                const int64_t lb = w_lab[s];
-                int rank = 0;
-                for (int j = 0; j < n && rank < k; ++j) rank += ranks_before_r(w_key[j], w_lab[j], kv, lb) ? 1 : 0;
-                if (rank < k) {
-                    o_key[rank] = kv;
-                    o_lab[rank] = lb;
-                    if (rank == k - 1) s_sk = kv;
-                }
-                const float r = fabsf(w_apx[s] - kv) / (B.bound_a(w_apx[s]) + B.bound_f(kv) + B.trunc(w_apx[s]));
-                atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
-            }
-            __syncthreads();
-            // +inf floor: no list dropped a row, so every row was a candidate and W holds all
-            // that can matter
-            const float tauL = key_from_ordered(w_tau);
-            ok = tauL == INFINITY || (tauL - B.bound_a(tauL)) > (s_sk + B.bound_f(s_sk));
-        }
-        if (ok) {
-            if (t < k) {
-                const int64_t lb = o_lab[t];
-                a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
-                                        : ((metric == 1) ? o_key[t] : -o_key[t]);
-                a.I[q * k + t] = lb;
-            }
-        } else if (t == 0) {
-            a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
-        }
-        __syncthreads();                // LDS reused by the next item
-    }
-}
-
-// Device-side exact re-run of the queries the certificate could not settle (no host round trip):
-// reads the uncertified count of this chunk (stats parity p), gathers those queries' padded rows
-// and norms (zero rows up to the next multiple of 32) and writes the launch plan the fused exact
-// kernel and the merge read from device memory: dyn = {count, query blocks, row splits, list
-// entries per query}.  Block 0 also folds this chunk's stats into the per-search accumulators and
-// zeroes the other parity for the next chunk (its previous user finished: stream order).
-__global__ void __launch_bounds__(256)
-fallback_prep_kernel(int* __restrict__ stat, int parity, int first, const int* __restrict__ list,
-                     const float* __restrict__ qpad, const float* __restrict__ qnorm, int dp,
-                     int grid_wgs, int ntiles, int lists_km, float* __restrict__ fq,
-                     float* __restrict__ fqn, int* __restrict__ dyn) {
-    const int* sp = stat + 4 * parity;
-    const int count = sp[0];
-    const int nqb = (count + 31) / 32;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const int nsplit = nqb ? max(1, min(grid_wgs / nqb, ntiles)) : 0;
-        dyn[0] = count;
-        dyn[1] = nqb;
-        dyn[2] = nsplit;
-        dyn[3] = nsplit * lists_km;
-        int* acc = stat + 8;
-        acc[0] = first ? sp[0] : acc[0] + sp[0];
-        acc[1] = first ? sp[1] : max(acc[1], sp[1]);        // ratio >= 0: bit order = float order
-        acc[2] = first ? sp[2] : acc[2] + sp[2];
-        int* other = stat + 4 * (parity ^ 1);
-        other[0] = 0; other[1] = 0; other[2] = 0; other[3] = 0;
-    }
-    const int lane = threadIdx.x & 63;
-    const int64_t rows = (int64_t)nqb * 32;
-    for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
-         row += (int64_t)gridDim.x * 4) {
-        float* o = fq + row * dp;
-        if (row >= count) {
-            for (int j = lane; j < dp; j += 64) o[j] = 0.f;
-            if (lane == 0) fqn[row] = 0.f;
-            continue;
-        }
-        const int src = list[row];
-        const float* s = qpad + (int64_t)src * dp;
-        for (int j = lane; j < dp; j += 64) o[j] = s[j];
-        if (lane == 0) fqn[row] = qnorm[src];
-    }
-}
-
 __global__ void __launch_bounds__(256)
 gather_rows_kernel(const float* __restrict__ src, const float* __restrict__ src_norm, int dp,
                    const int* __restrict__ list, int64_t n, int64_t n_pad,
@@ -648,19 +397,6 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     else if (a.dp <= 2048) IMGREC_RERANK(8);
     else IMGREC_RERANK(0);
 #undef IMGREC_RERANK
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !a.raw_d) return e;
-    const unsigned grid = (unsigned)std::min<int64_t>(a.nq, 256);
-    hipLaunchKernelGGL(second_chance_kernel, dim3(grid), dim3(kRerankWaves * 64), 0, st, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_fallback_prep(int* stat, int parity, int first, const int* list, const float* qpad,
-                                const float* qnorm, int dp, int grid_wgs, int ntiles, int lists_km,
-                                int64_t cap_rows, float* fq, float* fqn, int* dyn, hipStream_t st) {
-    const int64_t blocks = std::min<int64_t>(256, std::max<int64_t>(1, (cap_rows + 3) / 4));
-    hipLaunchKernelGGL(fallback_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, stat, parity,
-                       first, list, qpad, qnorm, dp, grid_wgs, ntiles, lists_km, fq, fqn, dyn);
     return hipGetLastError();
 }
 

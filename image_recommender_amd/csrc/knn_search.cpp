@@ -8,9 +8,9 @@
 //   split   split-bf16 candidate pass (three bf16 MFMAs per product) -> merge -> rerank +
 //           certificate (+ second chance).
 //
-// Queries no certificate settles are re-run exactly by a device-planned launch of the fused fp32
-// kernel (run_fallback): the count never travels to the host, so knn_search_device enqueues a
-// whole search without waiting for the GPU.
+// Queries no certificate settles are re-run exactly inside the certificate tail kernel, planned on
+// the device: the count never travels to the host, so knn_search_device enqueues a whole search
+// without waiting for the GPU.
 #include <cmath>
 #include <cstring>
 
@@ -87,56 +87,57 @@ int grow_stats(knn_index* ix, int64_t nq, hipStream_t st) {
     return grow(&ix->chance, &ix->chance_cap, (size_t)nq);
 }
 
-// Exact fp32 re-run of the queries this chunk's certificate left (list ix->fail, count in the
-// stats parity), planned on device: a fixed grid of (2,1) exact-kernel workgroups, those beyond
-// the plan exiting at once, then a merge that scatters each result row into place.  With nothing
-// to re-run it costs three near-empty launches.
-int run_fallback(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
-                 int64_t* I, hipStream_t st, int parity, bool first) {
-    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+// The rerank + certificate of a candidate chunk, then its whole tail in ONE launch
+// (cert_tail_kernel: second chance, stats fold, and the exact fp32 re-run of the queries neither
+// certificate settles — planned on the device, so the host never waits).  With every query
+// certified the tail is one near-empty launch.
+int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* qnorm, int64_t nq,
+                  int k, float* D, int64_t* I, hipStream_t st, bool first) {
+    const int parity = ix->stat_seq & 1;
     const int km = fallback_km(k);
-    const int grid = fallback_grid(ix->cus, nq);
+    const int grid = kTailWGPerCU * ix->cus;
     const int64_t cap_rows = round_up(nq, 32);
     const int bm = 128 * kFallbackWR;
-    const int ntiles = (int)((ix->ntotal + bm - 1) / bm);
     const int lists_km = 2 * kFallbackWR * km;
-    // candidate lists: at most `grid` (query block, row split) pairs of 32 queries each
+    // candidate lists: at most `grid` (query block, row split) items of 32 queries each
     const size_t ncap = (size_t)grid * 32 * lists_km;
     int rc;
     if ((rc = grow(&ix->fb_q, &ix->fb_q_cap, (size_t)cap_rows * ix->dp)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_qn, &ix->fb_qn_cap, (size_t)cap_rows)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_cd, &ix->fb_cd_cap, ncap)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_ci, &ix->fb_ci_cap, ncap)) != KNN_OK) return rc;
-    if (!ix->fb_dyn) KNN_HIP(hipMalloc((void**)&ix->fb_dyn, 4 * sizeof(int)));
-    KNN_HIP(launch_fallback_prep(ix->stat, parity, first ? 1 : 0, ix->fail, qpad, qnorm, ix->dp,
-                                 grid, ntiles, lists_km, cap_rows, ix->fb_q, ix->fb_qn, ix->fb_dyn,
-                                 st));
-    TileArgs a{};
-    a.wr = kFallbackWR; a.wq = 1; a.km = km; a.mode = kModeF32;
-    a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
-    a.qp = ix->fb_q; a.qnorm = ix->fb_qn; a.nq = 0; a.metric = kmetric;
-    a.ntiles = ntiles; a.nsplit = 0; a.nqb = 0; a.id_offset = ix->id_offset;
-    a.cand_d = ix->fb_cd; a.cand_i = ix->fb_ci; a.ncand = 0;
-    a.dyn = ix->fb_dyn; a.grid = grid;
-    KNN_HIP(launch_tile_topk(a, st));
-    KNN_HIP(launch_merge_dyn(ix->fb_cd, ix->fb_ci, ix->fb_dyn, 2 * kFallbackWR, km, nq, k, kmetric,
-                             ix->fail, D, I, st));
-    return KNN_OK;
-}
-
-// The rerank + certificate of a candidate chunk and the device-side exact re-run after it.
-int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* qnorm, int64_t nq,
-                  int k, float* D, int64_t* I, hipStream_t st, bool first) {
-    const int parity = ix->stat_seq & 1;
+    if ((rc = grow(&ix->tail_ctl, &ix->tail_ctl_cap, (size_t)4 + cap_rows / 32)) != KNN_OK) return rc;
     r.stats = ix->stat + 4 * parity;
     r.fail_list = ix->fail;
     r.chance_list = ix->chance;
+    r.tail_ctl = ix->tail_ctl;
     KNN_HIP(launch_rerank_certify(r, st));
-    const int rc = run_fallback(ix, qpad, qnorm, nq, k, D, I, st, parity, first);
-    if (rc != KNN_OK) {           // the parities may hold this chunk's counts: start clean
+    TailArgs t{};
+    t.r = r;
+    t.parity = parity;
+    t.first = first ? 1 : 0;
+    t.stat = ix->stat;
+    t.qpad = qpad;
+    t.qnorm = qnorm;
+    t.dp = ix->dp;
+    t.nrows = (int)ix->ntotal;
+    t.ntiles = (int)((ix->ntotal + bm - 1) / bm);
+    t.metric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    t.xb = ix->xb;
+    t.xn = ix->xn;
+    t.id_offset = ix->id_offset;
+    t.fq = ix->fb_q;
+    t.fqn = ix->fb_qn;
+    t.fcd = ix->fb_cd;
+    t.fci = ix->fb_ci;
+    t.ticket = ix->tail_ctl + 4;
+    t.km = km;
+    t.lists_km = lists_km;
+    const hipError_t e = launch_cert_tail(t, grid, st);
+    if (e != hipSuccess) {        // the parities may hold this chunk's counts: start clean
         (void)hipMemsetAsync(ix->stat, 0, 12 * sizeof(int), st);
         ix->stat_seq = 0;
-        return rc;
+        KNN_FAIL(KNN_EHIP, "certificate tail launch failed: %s", hipGetErrorString(e));
     }
     ++ix->stat_seq;
     ix->stat_valid = true;
@@ -322,9 +323,12 @@ int read_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int6
     if (!ix->stat_valid) return KNN_OK;
     int rc;
     if ((rc = fence_begin(ix, ix->stream)) != KNN_OK) return rc;
-    int acc[3] = {0, 0, 0};
+    int acc[4] = {0, 0, 0, 0};
     KNN_HIP(hipMemcpyAsync(acc, ix->stat + 8, sizeof(acc), hipMemcpyDeviceToHost, ix->stream));
     KNN_HIP(hipStreamSynchronize(ix->stream));
+    if (acc[3] != 0)          // cert_tail_kernel's bounded wait for its planner ran out
+        KNN_FAIL(KNN_EHIP, "certificate tail: a workgroup gave up waiting for the re-run plan "
+                           "(error bits 0x%x); results of that search are not certified", acc[3]);
     *fallback_q = acc[0];
     if (first_fail) *first_fail = acc[2];
     if (ratio) std::memcpy(ratio, &acc[1], sizeof(float));

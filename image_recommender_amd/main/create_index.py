@@ -27,14 +27,16 @@ import argparse
 import json
 import logging
 import os
+import queue
 import sqlite3
+import threading
 from pathlib import Path
 from types import SimpleNamespace
 
 import numpy as np
 
 from .. import faiss_compat as faiss
-from ..ingest import decode_rows
+from ..ingest import decode_rows, scan_native
 
 os.environ.setdefault("KMP_DUPLICATE_LIB_OK", "TRUE")
 
@@ -128,6 +130,70 @@ class FAISSIndexBuilderDB:
         """(ids, float32 matrix, part_dims) of the decodable rows, parts in caller order."""
         return decode_rows(rows, self.vector_types, part_dims, log=self._log)
 
+    # ---- the build's scan: native when the system SQLite library loads (§8f row 1) ------------
+    def _probe_part_dims(self, probe_rows=64):
+        select_cols, join_strs = self._make_select_and_joins()
+        rows = self.read_cur.execute(
+            f"SELECT {select_cols} FROM images i {join_strs} LIMIT {int(probe_rows)}").fetchall()
+        return decode_rows(rows, self.vector_types, None, log=lambda *a, **k: None)[2]
+
+    def _refetch(self, ids):
+        select_cols, join_strs = self._make_select_and_joins()
+        out = []
+        for i in range(0, len(ids), 900):            # SQLite's bound-variable limit
+            chunk = ids[i:i + 900]
+            out += self.read_conn.execute(
+                f"SELECT {select_cols} FROM images i {join_strs} WHERE i.id IN "
+                f"({','.join('?' * len(chunk))})", chunk).fetchall()
+        return out
+
+    def _decoded_batches(self):
+        """(ids, float32 matrix, part_dims) per batch of the scan, in the query's row order.
+
+        Native path (ingest.scan_native: the same SELECT stepped from C, BLOBs parsed in place)
+        on a producer thread, so the scan of batch i+1 overlaps the index add of batch i (both
+        release the GIL); rows it cannot parse are re-read and decoded by _process_batch's pickle
+        fallback.  Without the native scan: _batch_records + _process_batch (the reference's
+        loop, create_index.py:136-189, with the batch decode in C)."""
+        part_dims = self._probe_part_dims()
+        if part_dims is not None:
+            select_cols, join_strs = self._make_select_and_joins()
+            sql = f"SELECT {select_cols} FROM images i {join_strs}"
+            try:
+                gen = scan_native(self.db_path, sql, self.vector_types, part_dims, self.batch_size,
+                                  self._refetch, log=self._log)
+                first = next(gen, None)
+            except NotImplementedError as e:
+                self._log(f"native scan unavailable ({e}); scanning in Python", level="warning")
+                gen = None
+            if gen is not None:
+                if first is None:
+                    return
+                q: queue.Queue = queue.Queue(maxsize=2)
+
+                def produce():
+                    try:
+                        for item in gen:
+                            q.put(item)
+                        q.put(None)
+                    except BaseException as e:   # noqa: BLE001 - re-raised on the consumer side
+                        q.put(e)
+                t = threading.Thread(target=produce, daemon=True)
+                t.start()
+                yield first[0], first[1], part_dims
+                while True:
+                    item = q.get()
+                    if item is None:
+                        break
+                    if isinstance(item, BaseException):
+                        raise item
+                    yield item[0], item[1], part_dims
+                t.join()
+                return
+        for batch in self._batch_records():
+            ids, arr, part_dims = self._process_batch(batch, part_dims)
+            yield ids, arr, part_dims
+
     # ---- index (create_index.py:191-234) -------------------------------------------------------
     def find_valid_m(self, dim, candidates=(64, 56, 48, 32, 28, 24, 16, 12, 8)):
         for m in candidates:
@@ -187,9 +253,8 @@ class FAISSIndexBuilderDB:
         part_dims = None
         offset_counter = 0
         batch_num = 0
-        for batch in self._batch_records():
+        for ids, arr, part_dims in self._decoded_batches():
             batch_num += 1
-            ids, arr, part_dims = self._process_batch(batch, part_dims)
             if len(ids) == 0:
                 continue
             if index is None:

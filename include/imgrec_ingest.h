@@ -36,6 +36,22 @@ int64_t ingest_concat_packed(const uint8_t* buf, const int64_t* offsets, const i
                              int64_t nrows, int nparts, const int64_t* part_dims, float* out,
                              int8_t* status);
 
+/* Native scan of the index builder's query (the reference's _batch_records + _process_batch,
+ * /root/reference/main/create_index.py:136-189, in one pass): `sql` = "SELECT id, blob_1 .. blob_P
+ * FROM ..." is run read-only on db_path through the system SQLite library (libsqlite3.so.0,
+ * dlopen'd: the library Python's sqlite3 module uses, hence the same plan and row order), and
+ * every row's BLOBs are parsed in place.  ingest_scan_next fills up to cap rows: ids[i], the
+ * concatenated float32 row out[i * sum(part_dims) ...] and status[i] as ingest_concat_rows (rows
+ * with status != 0 are left to the caller's pickle fallback).  Returns the rows filled, 0 at the
+ * end, < 0 on an SQLite error (message: ingest_scan_error). */
+typedef struct ingest_scan ingest_scan_t;
+int ingest_scan_open(const char* db_path, const char* sql, int nparts, const int64_t* part_dims,
+                     ingest_scan_t** out);
+int64_t ingest_scan_next(ingest_scan_t* scan, int64_t cap, int64_t* ids, float* out,
+                         int8_t* status);
+int ingest_scan_close(ingest_scan_t* scan);
+const char* ingest_scan_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,3 +20,5 @@ for i in 1 2; do timeout -k 10 120 python bench.py --rows 125000 --profile-only 
 cat $OUT/rows125k.jsonl
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $OUT/prof125k -o run --output-format csv -- python3 bench.py --rows 125000 --profile-only --steps 50 --warmup 5 > $OUT/prof125k.log 2>&1 || { tail $OUT/prof125k.log; exit 4; }
 grep elapsed $OUT/prof125k.log
+timeout -k 10 600 python tools/bench_ingest.py --rows ${INGEST_ROWS:-1000000} > $OUT/ingest.json 2> $OUT/ingest.err || { echo "ingest failed"; tail -5 $OUT/ingest.err; exit 5; }
+cut -c1-600 $OUT/ingest.json
