@@ -87,7 +87,41 @@ __global__ void __launch_bounds__(256) quick_gelu_kernel(uint16_t* __restrict__ 
     }
 }
 
+// nn.GELU (erf form) in place: 16 bf16 per thread (two 16-B loads in flight), fp32 inside.
+__device__ __forceinline__ uint32_t gelu2(uint32_t p) {
+    const float a = __uint_as_float(p << 16), c = __uint_as_float(p & 0xffff0000u);
+    const uint32_t lo = f32_to_bf16(0.5f * a * (1.f + erff(a * 0.70710678118654752f)));
+    const uint32_t hi = f32_to_bf16(0.5f * c * (1.f + erff(c * 0.70710678118654752f)));
+    return lo | (hi << 16);
+}
+
+__global__ void __launch_bounds__(256) gelu_kernel(uint16_t* __restrict__ h, int64_t n) {
+    const int64_t i16 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i16 + 16 <= n) {
+        uint4 w0 = *reinterpret_cast<const uint4*>(h + i16);
+        uint4 w1 = *reinterpret_cast<const uint4*>(h + i16 + 8);
+        w0 = make_uint4(gelu2(w0.x), gelu2(w0.y), gelu2(w0.z), gelu2(w0.w));
+        w1 = make_uint4(gelu2(w1.x), gelu2(w1.y), gelu2(w1.z), gelu2(w1.w));
+        *reinterpret_cast<uint4*>(h + i16) = w0;
+        *reinterpret_cast<uint4*>(h + i16 + 8) = w1;
+    } else {
+        for (int64_t i = i16; i < n; ++i) {
+            const float a = bf16_to_f32(h[i]);
+            h[i] = f32_to_bf16(0.5f * a * (1.f + erff(a * 0.70710678118654752f)));
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int vit_gelu_bf16(uint16_t* h, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && !h) || ((uintptr_t)h & 15)) return -1;
+    if (n == 0) return 0;
+    const int64_t threads = (n + 15) / 16;
+    hipLaunchKernelGGL(gelu_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, h, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int vit_add_layernorm_bf16(float* x, const uint16_t* delta, const float* gamma,
                                       const float* beta, uint16_t* y, int64_t rows, int dim,

@@ -138,13 +138,19 @@ class FAISSIndexBuilderDB:
         return decode_rows(rows, self.vector_types, None, log=lambda *a, **k: None)[2]
 
     def _refetch(self, ids):
+        """The (id, blob...) rows of `ids` (rows the native scan could not parse), on a
+        connection of the calling thread (the scan's producer thread)."""
         select_cols, join_strs = self._make_select_and_joins()
         out = []
-        for i in range(0, len(ids), 900):            # SQLite's bound-variable limit
-            chunk = ids[i:i + 900]
-            out += self.read_conn.execute(
-                f"SELECT {select_cols} FROM images i {join_strs} WHERE i.id IN "
-                f"({','.join('?' * len(chunk))})", chunk).fetchall()
+        con = sqlite3.connect(self.db_path)
+        try:
+            for i in range(0, len(ids), 900):            # SQLite's bound-variable limit
+                chunk = ids[i:i + 900]
+                out += con.execute(
+                    f"SELECT {select_cols} FROM images i {join_strs} WHERE i.id IN "
+                    f"({','.join('?' * len(chunk))})", chunk).fetchall()
+        finally:
+            con.close()
         return out
 
     def _decoded_batches(self):

@@ -99,6 +99,30 @@ def _add_ln(x, delta, ln):
     return y
 
 
+def _lin_gelu(m, x):
+    """GELU(x W^T + b) of a prepared Linear in ONE hipBLASLt launch (GELU_BIAS epilogue through
+    torch._addmm_activation).  The epilogue's GELU is the tanh form; against the erf form of
+    nn.GELU it differs by < 5e-4 absolute (< 2e-4 relative), below the bf16 rounding of the
+    output it is applied to (2^-9 relative)."""
+    import torch
+    shp = x.shape
+    y = torch._addmm_activation(m.b_lp, x.reshape(-1, shp[-1]), m.w_lp.t(), use_gelu=True)
+    return y.view(*shp[:-1], y.shape[-1])
+
+
+def _gelu_(h):
+    """nn.GELU (erf form) in place on a contiguous bf16 tensor (vit_gelu_bf16)."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    rc = _lib.load().vit_gelu_bf16(C.c_void_p(h.data_ptr()), h.numel(),
+                                   C.c_void_p(torch.cuda.current_stream(h.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_gelu_bf16 failed")
+    return h
+
+
 def _quick_gelu_(h):
     """CLIP's QuickGELU in place on a contiguous bf16 tensor (vit_quick_gelu_bf16)."""
     import ctypes as C
@@ -144,8 +168,13 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             qkv = _lin(self.qkv, _add_ln(x, delta, self.ln1)).view(b, n, 3, self.heads, c // self.heads)
             q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
             a = F.scaled_dot_product_attention(q, k, v)
-            h = _lin(self.fc1, _add_ln(x, _lin(self.proj, a.transpose(1, 2).reshape(b, n, c)), self.ln2))
-            h = _quick_gelu_(h) if self.quick_gelu else F.gelu(h)
+            y = _add_ln(x, _lin(self.proj, a.transpose(1, 2).reshape(b, n, c)), self.ln2)
+            if self.quick_gelu:
+                h = _quick_gelu_(_lin(self.fc1, y))
+            elif getattr(self, "gelu_epilogue", False):
+                h = _lin_gelu(self.fc1, y)
+            else:
+                h = _gelu_(_lin(self.fc1, y))
             return _lin(self.fc2, h)
 
     class ViT(nn.Module):
@@ -210,13 +239,16 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             parts = [F.normalize(t(x).float(), dim=-1) for t in self.towers]
             return torch.cat(parts, -1)
 
-        def prepare_inference(self, dtype, fused=False):
+        def prepare_inference(self, dtype, fused=False, gelu_epilogue=False):
             """Cache low-precision copies of every matrix-product weight once (autocast would
             re-cast them on every forward); LayerNorms and the residual stream stay fp32.
             fused (bf16, on a GPU): residual add + LayerNorm + bf16 cast and QuickGELU run as
-            single HIP passes (include/imgrec_vit.h)."""
+            single HIP passes (include/imgrec_vit.h).  gelu_epilogue (with fused): the erf
+            GELU after fc1 becomes the GEMM's own epilogue (_lin_gelu)."""
             for t in self.towers:
                 t.fused = bool(fused) and dtype == torch.bfloat16
+                for blk in t.blocks:
+                    blk.gelu_epilogue = t.fused and bool(gelu_epilogue)
             for m in self.modules():
                 if isinstance(m, (nn.Linear, nn.Conv2d)):
                     w = m.weight.detach()

@@ -27,6 +27,10 @@ int vit_add_layernorm_bf16(float* x, const uint16_t* delta, const float* gamma, 
 /* In place on n bf16 values: h = bf16(h * sigmoid(1.702 h)) (CLIP's QuickGELU), fp32 inside. */
 int vit_quick_gelu_bf16(uint16_t* h, int64_t n, void* stream);
 
+/* In place on n bf16 values: h = bf16(0.5 h (1 + erf(h / sqrt 2))) (nn.GELU, the DINO and
+ * OpenCLIP towers' MLP activation), fp32 inside. */
+int vit_gelu_bf16(uint16_t* h, int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

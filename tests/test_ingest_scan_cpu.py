@@ -94,3 +94,23 @@ def test_native_scan_reports_sql_errors(tmp_path):
     _make_db(db, n=10)
     with pytest.raises(RuntimeError, match="sqlite3_prepare_v2"):
         list(ingest.scan_native(str(db), "SELECT nope FROM nowhere", TYPES, DIMS, 8, lambda ids: []))
+
+
+def test_builder_decoded_batches_native_equals_reference_loop(tmp_path, monkeypatch):
+    """FAISSIndexBuilderDB._decoded_batches (native scan on a producer thread, refetch of the
+    rows it cannot parse on that thread's own connection) yields what the reference-shaped loop
+    (_batch_records + _process_batch) yields."""
+    from image_recommender_amd.main.create_index import FAISSIndexBuilderDB
+    db = tmp_path / "images.db"
+    _make_db(db, n=2500)
+    monkeypatch.chdir(tmp_path)
+    b = FAISSIndexBuilderDB(db_path=str(db), vector_types=TYPES, batch_size=700,
+                            log_dir=str(tmp_path / "logs"))
+    got = [(list(ids), arr) for ids, arr, _ in b._decoded_batches()]
+    ref = []
+    dims = None
+    for rows in b._batch_records():
+        ids, arr, dims = b._process_batch(rows, dims)
+        ref.append((list(ids), arr))
+    assert [i for ids, _ in got for i in ids] == [i for ids, _ in ref for i in ids]
+    np.testing.assert_array_equal(np.concatenate([a for _, a in got]), np.concatenate([a for _, a in ref]))

@@ -47,3 +47,38 @@ def test_fused_forward_matches_unfused(gpu):
         b = torch.nn.functional.normalize(fused.embed(x).float(), dim=-1)
     cos = (a * b).sum(-1)
     assert float(cos.min()) > 0.999, cos
+
+
+def test_gelu_matches_torch(gpu):
+    """vit_gelu_bf16 (erf form, in place) against torch's fp32 erf GELU: within one bf16 rounding."""
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import _gelu_
+    for n in (3 * 197 * 3072 + 11, 16, 5):                      # whole 16-element groups and tails
+        h = (torch.randn(n, device="cuda") * 4).bfloat16()
+        ref = torch.nn.functional.gelu(h.float())
+        out = _gelu_(h.clone())
+        torch.cuda.synchronize()
+        err = (out.float() - ref).abs()
+        assert float((err - ref.abs() * 2.0 ** -8 - 1e-6).max()) <= 0.0
+
+
+def test_gelu_epilogue_within_bf16_of_erf_gelu(gpu):
+    """The fc1 + GELU as one hipBLASLt launch (GELU_BIAS epilogue, tanh form; _lin_gelu) against
+    the fp32 erf-form reference of the same bf16 GEMM: within 2 bf16 roundings (the tanh-erf gap
+    is < 5e-4 absolute); and the forward built on it against the unfused forward, cos > 0.999."""
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import _lin_gelu, build_ensemble
+    g = torch.Generator(device="cuda").manual_seed(3)
+    lin = torch.nn.Linear(768, 3072).cuda()
+    lin.w_lp, lin.b_lp = lin.weight.detach().bfloat16(), lin.bias.detach().bfloat16()
+    x = torch.randn(2, 197, 768, device="cuda", generator=g).bfloat16()
+    ref = torch.nn.functional.gelu(torch.nn.functional.linear(x.float(), lin.w_lp.float(), lin.b_lp.float()))
+    got = _lin_gelu(lin, x).float()
+    err = (got - ref).abs()
+    assert float((err - ref.abs() * 2.0 ** -7 - 2e-3).max()) <= 0.0
+    xi = torch.rand((4, 3, 224, 224), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    plain = build_ensemble(seed=0, depth=4).cuda().eval().prepare_inference(torch.bfloat16)
+    lt = build_ensemble(seed=0, depth=4).cuda().eval().prepare_inference(torch.bfloat16, fused=True,
+                                                                          gelu_epilogue=True)
+    with torch.no_grad():
+        a = torch.nn.functional.normalize(plain.embed(xi).float(), dim=-1)
+        b = torch.nn.functional.normalize(lt.embed(xi).float(), dim=-1)
+    assert float((a * b).sum(-1).min()) > 0.999
