@@ -984,19 +984,30 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
         return c;
     };
     int nvl = 0;
+    uint64_t vmin = kEmpty, vmax = 0;
 #pragma unroll
-    for (int p = 0; p < KIN; ++p) nvl += v[p] != kEmpty ? 1 : 0;
+    for (int p = 0; p < KIN; ++p) {
+        const bool val = v[p] != kEmpty;
+        nvl += val ? 1 : 0;
+        vmin = v[p] < vmin ? v[p] : vmin;
+        vmax = (val && v[p] > vmax) ? v[p] : vmax;
+    }
     const int K = min(kout, wave_sum_i32(nvl));
     uint64_t T = 0;
     if (K > 0) {
-        uint64_t prefix = 0;
-        for (int b = 63; b >= 32; --b) {
+        // T lies in [min, max] of the valid values: the bits above their highest difference are
+        // common, so the select starts below them (keys of one query sit in a narrow range)
+        vmin = wave_min_u64(vmin);
+        vmax = ~wave_min_u64(~vmax);
+        const int hb = vmin == vmax ? -1 : 63 - __builtin_clzll(vmin ^ vmax);
+        uint64_t prefix = hb < 0 ? vmin : (hb >= 63 ? 0 : vmin & ~((2ull << hb) - 1));
+        for (int b = min(hb, 63); b >= 32; --b) {
             const uint64_t lo = prefix | ((1ull << b) - 1);
             if (wave_sum_i32(count_le(lo)) < K) prefix |= 1ull << b;
         }
         T = prefix | 0xffffffffull;
         if (wave_sum_i32(count_le(T)) > K) {                   // the K-th key is tied: rows decide
-            for (int b = 31; b >= 0; --b) {
+            for (int b = min(hb, 31); b >= 0; --b) {
                 const uint64_t lo = prefix | ((1ull << b) - 1);
                 if (wave_sum_i32(count_le(lo)) < K) prefix |= 1ull << b;
             }
@@ -1024,43 +1035,126 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
     }
 }
 
-// Second level of the two-level merge: up to 64 packed lists of up to 64 entries per query, the
-// lane queues in LDS with a head index each (one wave per query).  Inputs are the first level's
-// outputs: (key, global label) sorted ascending, plus G floors per query.
-__global__ void __launch_bounds__(64)
-cand_merge_lds_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
-                      int nlists, int kin, int kout, int64_t id_offset,
-                      const float* __restrict__ floor_in, float* __restrict__ D,
-                      int64_t* __restrict__ I, float* __restrict__ floor_out) {
-    __shared__ uint64_t qv[64 * 65];                  // lane l's queue at qv[l * 65 ...]
-    const int lane = threadIdx.x;
-    const int64_t q = blockIdx.x;
-    constexpr uint64_t kEmpty = ~0ull;
-    float fl = lane < nlists ? floor_in[q * nlists + lane] : INFINITY;
-    if (lane < nlists) {
-        const float* lp = cd + (q * nlists + lane) * kin;
-        const int64_t* ip = ci + (q * nlists + lane) * kin;
-        for (int p = 0; p < kin; ++p) {
-            const int64_t lab = ip[p];
-            qv[lane * 65 + p] = lab < 0 ? kEmpty
-                                        : ((uint64_t)key_bits_ordered(lp[p]) << 32) | (uint32_t)(lab - id_offset);
-        }
-        if (ip[kin - 1] >= 0) fl = fminf(fl, lp[kin - 1]);
-    }
-    for (int p = (lane < nlists ? kin : 0); p <= 64; ++p) qv[lane * 65 + p] = kEmpty;
+// Second level of the two-level merge (round 3): one 256-thread block per query takes the G <= 64
+// first-level outputs (sorted (key, global label) lists of kin <= 64 entries + G floors), packs
+// them as (order-preserving key bits | local row) u64 in registers (<= 16 per thread), and finds
+// the K = min(kout, valid) smallest by the same bit-by-bit threshold select as the first level,
+// with block-wide counts (32 steps over the key bits; the row bits only when the K-th key is
+// tied).  The K winners are compacted by a block scan and each placed at its rank.  Replaces a
+// one-wave LDS-queue merge (kout rounds of a wave minimum, each behind a dependent LDS read):
+// 32.5 us per query at nq = 1 (profiles/r03/).
+constexpr int kMergeBlockThreads = 256, kMergeBlockPer = 16;    // <= 4096 entries per query
+
+__device__ __forceinline__ int block_sum_i32(int x, int* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int w = wave_sum_i32(x);
+    if (lane == 0) red[wave] = w;
     __syncthreads();
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < kMergeBlockThreads / 64; ++i) tot += red[i];
+    __syncthreads();                                  // red reused by the next call
+    return tot;
+}
+
+__global__ void __launch_bounds__(kMergeBlockThreads)
+cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
+                        int nlists, int kin, int kout, int64_t id_offset,
+                        const float* __restrict__ floor_in, float* __restrict__ D,
+                        int64_t* __restrict__ I, float* __restrict__ floor_out) {
+    __shared__ int red[kMergeBlockThreads / 64];
+    __shared__ float redf[kMergeBlockThreads / 64];
+    __shared__ uint64_t sel[64];
+    constexpr uint64_t kEmpty = ~0ull;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int64_t q = blockIdx.x;
+    const int M = nlists * kin;
+    __shared__ uint64_t redm[2][kMergeBlockThreads / 64];
+    uint64_t v[kMergeBlockPer];
+    int nvl = 0;
+    uint64_t vmin = kEmpty, vmax = 0;
+#pragma unroll
+    for (int j = 0; j < kMergeBlockPer; ++j) {
+        const int e = t + j * kMergeBlockThreads;
+        v[j] = kEmpty;
+        if (e < M) {
+            const int64_t lab = ci[q * M + e];
+            if (lab >= 0) {
+                v[j] = ((uint64_t)key_bits_ordered(cd[q * M + e]) << 32) | (uint32_t)(lab - id_offset);
+                ++nvl;
+                vmin = v[j] < vmin ? v[j] : vmin;
+                vmax = v[j] > vmax ? v[j] : vmax;
+            }
+        }
+    }
+    vmin = wave_min_u64(vmin);
+    vmax = ~wave_min_u64(~vmax);
+    if (lane == 0) { redm[0][wave] = vmin; redm[1][wave] = vmax; }
+    // floor: the first level's floors and the last key of every full first-level list
+    float fl = INFINITY;
+    if (t < nlists) {
+        fl = floor_in[q * nlists + t];
+        const int64_t last = (q * nlists + t) * kin + kin - 1;
+        if (ci[last] >= 0) fl = fminf(fl, cd[last]);
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
-    if (lane == 0) floor_out[q] = fl;
-    int head = 0;
-    uint64_t cur = qv[lane * 65];
-    for (int r = 0; r < kout; ++r) {
-        const uint64_t b = wave_min_u64(cur);
-        if (b != kEmpty && cur == b) cur = qv[lane * 65 + (++head)];
-        if (lane == 0) {
-            D[q * kout + r] = b == kEmpty ? FLT_MAX : key_from_ordered((uint32_t)(b >> 32));
-            I[q * kout + r] = b == kEmpty ? (int64_t)-1 : (int64_t)(uint32_t)b + id_offset;
+    if (lane == 0) redf[wave] = fl;
+    auto count_le = [&](uint64_t x) __attribute__((always_inline)) {
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < kMergeBlockPer; ++j) c += v[j] <= x ? 1 : 0;
+        return c;
+    };
+    const int K = min(kout, block_sum_i32(nvl, red));   // (its barrier also publishes redf)
+    if (t == 0) {
+        float f = redf[0];
+#pragma unroll
+        for (int i = 1; i < kMergeBlockThreads / 64; ++i) f = fminf(f, redf[i]);
+        floor_out[q] = f;
+    }
+    uint64_t T = 0;
+    if (K > 0) {
+        // bits above the highest difference of the valid values' min and max are common to T
+        for (int i = 0; i < kMergeBlockThreads / 64; ++i) {
+            vmin = redm[0][i] < vmin ? redm[0][i] : vmin;
+            vmax = redm[1][i] > vmax ? redm[1][i] : vmax;
         }
+        const int hb = vmin == vmax ? -1 : 63 - __builtin_clzll(vmin ^ vmax);
+        uint64_t prefix = hb < 0 ? vmin : (hb >= 63 ? 0 : vmin & ~((2ull << hb) - 1));
+        for (int b = min(hb, 63); b >= 32; --b) {
+            const uint64_t lo = prefix | ((1ull << b) - 1);
+            if (block_sum_i32(count_le(lo), red) < K) prefix |= 1ull << b;
+        }
+        T = prefix | 0xffffffffull;
+        if (block_sum_i32(count_le(T), red) > K) {        // the K-th key is tied: rows decide
+            for (int b = min(hb, 31); b >= 0; --b) {
+                const uint64_t lo = prefix | ((1ull << b) - 1);
+                if (block_sum_i32(count_le(lo), red) < K) prefix |= 1ull << b;
+            }
+            T = prefix;
+        }
+    }
+    // compaction of the K winners (values are distinct: a row sits in one list)
+    const int c = K > 0 ? count_le(T) : 0;
+    const int wex = wave_excl_scan_i32(c);
+    if (lane == 63) red[wave] = wex + c;
+    __syncthreads();
+    int base = wex;
+    for (int i = 0; i < wave; ++i) base += red[i];
+#pragma unroll
+    for (int j = 0; j < kMergeBlockPer; ++j)
+        if (v[j] <= T && K > 0) sel[base++] = v[j];
+    __syncthreads();
+    if (t < K) {
+        const uint64_t mine = sel[t];
+        int rank = 0;
+        for (int j = 0; j < K; ++j) rank += sel[j] < mine ? 1 : 0;
+        D[q * kout + rank] = key_from_ordered((uint32_t)(mine >> 32));
+        I[q * kout + rank] = (int64_t)(uint32_t)mine + id_offset;
+    } else if (t < kout) {
+        D[q * kout + t] = FLT_MAX;
+        I[q * kout + t] = -1;
     }
 }
 
@@ -1091,14 +1185,15 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
         else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        // Level 2 (the G group outputs) is the LDS queue merge, 31 us per query at nq = 1.
-        // Measured and dropped: the threshold select with a group's 64 outputs per lane
+        // Level 2 (the G group outputs): the block-wide threshold select above.  Round 2's
+        // one-wave LDS-queue merge took 31-32.5 us per query at nq = 1; also measured and
+        // dropped then: the threshold select with a group's 64 outputs per lane of ONE wave
         // (cand_merge_lane_kernel<64>, 32.5 us), reading each queue's next entry one pop ahead
         // (32.3 us), and a 256-thread rank form (binary searches of every entry in every other
         // queue, 123 us: dependent LDS reads per thread).
 #undef IMGREC_CAND_LANE
-        hipLaunchKernelGGL(cand_merge_lds_kernel, dim3((unsigned)nq), dim3(64), 0, st, ws_d, ws_i, nq,
-                           G, kout, kout, id_offset, ws_floor, D, I, floor);
+        hipLaunchKernelGGL(cand_merge_block_kernel, dim3((unsigned)nq), dim3(kMergeBlockThreads), 0, st,
+                           ws_d, ws_i, nq, G, kout, kout, id_offset, ws_floor, D, I, floor);
         return hipGetLastError();
     }
     // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is

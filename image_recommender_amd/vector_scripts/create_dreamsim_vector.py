@@ -110,6 +110,46 @@ def _lin_gelu(m, x):
     return y.view(*shp[:-1], y.shape[-1])
 
 
+def _patchify(img, mean, std, p):
+    """(B, 3, H, W) fp32 image -> bf16 GEMM rows (B, (H/p)(W/p), 3 p p) of ((img - mean) / std),
+    patches laid out (c, kh, kw) — one HIP pass (vit_patchify_bf16) for the normalisation, the
+    patch permute and the bf16 cast."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    img = img.contiguous().float()
+    b, c, h, w = img.shape
+    out = torch.empty((b, (h // p) * (w // p), c * p * p), dtype=torch.bfloat16, device=img.device)
+    mean, std = mean.contiguous(), std.contiguous()
+    rc = _lib.load().vit_patchify_bf16(C.c_void_p(img.data_ptr()), b, h, w, p,
+                                       C.c_void_p(mean.data_ptr()), C.c_void_p(std.data_ptr()),
+                                       C.c_void_p(out.data_ptr()),
+                                       C.c_void_p(torch.cuda.current_stream(img.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_patchify_bf16 failed")
+    return out
+
+
+def _tokens(pe, cls, pos):
+    """bf16 patch embeddings (B, np, C) -> fp32 tokens (B, np + 1, C) = cat(cls, pe) + pos in one
+    HIP pass (vit_tokens_f32)."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    pe = pe.contiguous()
+    b, n, c = pe.shape
+    cls, pos = cls.detach().contiguous(), pos.detach().contiguous()
+    out = torch.empty((b, n + 1, c), dtype=torch.float32, device=pe.device)
+    rc = _lib.load().vit_tokens_f32(C.c_void_p(pe.data_ptr()), C.c_void_p(cls.data_ptr()),
+                                    C.c_void_p(pos.data_ptr()), b, n, c, C.c_void_p(out.data_ptr()),
+                                    C.c_void_p(torch.cuda.current_stream(pe.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_tokens_f32 failed")
+    return out
+
+
 def _gelu_(h):
     """nn.GELU (erf form) in place on a contiguous bf16 tensor (vit_gelu_bf16)."""
     import ctypes as C
@@ -197,8 +237,18 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             nn.init.normal_(self.cls, std=0.02)
 
         def forward(self, x):                      # x: (B, 3, 224, 224) in [0, 1]
-            x = (x - self.mean) / self.std
             w = getattr(self.patch, "w_lp", None)
+            if getattr(self, "fused", False) and w is not None:
+                # normalisation + patch extraction, the patch GEMM, then cls / pos in one pass
+                p = self.patch.kernel_size[0]
+                t = F.linear(_patchify(x, self.mean, self.std, p), w, self.patch.b_lp)
+                x = self.ln_pre(_tokens(t, self.cls, self.pos))
+                delta = None
+                for blk in self.blocks:
+                    delta = blk.forward_fused(x, delta)
+                x = self.ln_post(x[:, 0] + delta[:, 0].float())
+                return x if isinstance(self.head, nn.Identity) else _lin(self.head, x)
+            x = (x - self.mean) / self.std
             if w is None:
                 x = self.patch(x).flatten(2).transpose(1, 2)
             else:
@@ -211,13 +261,6 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
                 x = x.float()
             x = torch.cat([self.cls.expand(x.shape[0], -1, -1), x], 1) + self.pos
             x = self.ln_pre(x)
-            if getattr(self, "fused", False):
-                x = x.contiguous()
-                delta = None
-                for blk in self.blocks:
-                    delta = blk.forward_fused(x, delta)
-                x = self.ln_post(x[:, 0] + delta[:, 0].float())
-                return x if isinstance(self.head, nn.Identity) else _lin(self.head, x)
             for blk in self.blocks:
                 x = blk(x)
             x = self.ln_post(x[:, 0])
@@ -339,7 +382,7 @@ class DreamSimVectorIndexer(BaseVectorIndexer):
                                "downloads them at run time; pass weights_path=...)")
         self.model = model.to(self.device).eval()
         if self.device.type == "cuda":       # bf16 products + the fused HIP elementwise passes
-            self.model.prepare_inference(torch.bfloat16, fused=True)
+            self.model.prepare_inference(torch.bfloat16, fused=True, gelu_epilogue=True)
         self.dim = model.dim
         self._log_and_print("DreamSim model loaded and warmed up.", level="info")
 

@@ -31,6 +31,17 @@ int vit_quick_gelu_bf16(uint16_t* h, int64_t n, void* stream);
  * OpenCLIP towers' MLP activation), fp32 inside. */
 int vit_gelu_bf16(uint16_t* h, int64_t n, void* stream);
 
+/* The tower input as GEMM rows: image (batch, 3, height, width) fp32 -> bf16(((x - mean[c]) /
+ * std[c])) patches (batch, (height/patch)(width/patch), 3 patch patch), each laid out (c, kh, kw)
+ * like the stride-`patch` patch conv's weight (patch a multiple of 8; 16-B aligned pointers). */
+int vit_patchify_bf16(const float* img, int64_t batch, int height, int width, int patch,
+                      const float* mean, const float* std_, uint16_t* out, void* stream);
+
+/* Token rows: out (batch, npatch + 1, dim) fp32 = [cls + pos[0] ; fp32(patch_emb[b]) + pos[1:]]
+ * (patch_emb bf16 (batch, npatch, dim); dim a multiple of 4; 16-B aligned fp32 pointers). */
+int vit_tokens_f32(const uint16_t* patch_emb, const float* cls, const float* pos, int64_t batch,
+                   int npatch, int dim, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

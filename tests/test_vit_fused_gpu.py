@@ -6,7 +6,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("rows,dim", [(1, 64), (197 * 3, 768), (50, 1000), (7, 300)])
+@pytest.mark.parametrize("rows,dim", [(1, 64), (197 * 3, 768), (50, 1000), (7, 300), (5, 1024), (9, 256)])
 @pytest.mark.parametrize("with_delta", [True, False])
 def test_add_layernorm_matches_torch(gpu, rows, dim, with_delta):
     from image_recommender_amd.vector_scripts.create_dreamsim_vector import _add_ln
@@ -82,3 +82,25 @@ def test_gelu_epilogue_within_bf16_of_erf_gelu(gpu):
         a = torch.nn.functional.normalize(plain.embed(xi).float(), dim=-1)
         b = torch.nn.functional.normalize(lt.embed(xi).float(), dim=-1)
     assert float((a * b).sum(-1).min()) > 0.999
+
+
+def test_patchify_and_tokens_match_torch(gpu):
+    """vit_patchify_bf16 = bf16((x - mean) / std) in the conv weight's (c, kh, kw) patch layout, and
+    vit_tokens_f32 = cat(cls, pe.float()) + pos — both bit-exact against the torch ops they fuse."""
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import _patchify, _tokens
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.rand((3, 3, 224, 224), device="cuda", generator=g)
+    mean = torch.tensor((0.48, 0.45, 0.40), device="cuda").view(1, 3, 1, 1)
+    std = torch.tensor((0.26, 0.26, 0.27), device="cuda").view(1, 3, 1, 1)
+    p = 16
+    ref = ((x - mean) / std).bfloat16().reshape(3, 3, 14, p, 14, p).permute(0, 2, 4, 1, 3, 5)
+    ref = ref.reshape(3, 196, 3 * p * p)
+    got = _patchify(x, mean, std, p)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    pe = torch.randn((3, 196, 768), device="cuda", generator=g).bfloat16()
+    cls = torch.randn((1, 1, 768), device="cuda", generator=g)
+    pos = torch.randn((1, 197, 768), device="cuda", generator=g)
+    tok = _tokens(pe, cls, pos)
+    torch.cuda.synchronize()
+    assert torch.equal(tok, torch.cat([cls.expand(3, -1, -1), pe.float()], 1) + pos)

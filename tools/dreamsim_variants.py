@@ -11,6 +11,7 @@ images/s of variants on one GPU, random weights, bf16 autocast, 224 x 224 inputs
   fused      residual add + LayerNorm + bf16 cast and QuickGELU as single HIP passes
              (include/imgrec_vit.h)
   fused_gelu_lt  fused + fc1's GELU as the hipBLASLt GELU_BIAS epilogue (torch._addmm_activation)
+  X@B        variant X with SDPA restricted to backend B (flash / efficient / math)
 
 FLOP per image: 3 ViT-B/16 towers at 224 (197 tokens): 2 x 17.58 GMAC each -> 105.5 GFLOP;
 bf16 MFMA fraction = images/s x 105.5 GFLOP / 2516.8 TFLOP/s.  Prints one JSON line per variant.
@@ -51,7 +52,7 @@ def main():
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
                 return torch.nn.functional.normalize(model.embed(x).float(), dim=-1)
         with torch.no_grad():                          # weights cast once (the shipped form)
-            m = {"fused": fused, "fused_gelu_lt": fused_lt}.get(var_now[0], cached)
+            m = {"fused": fused, "fused_gelu_lt": fused_lt}.get(var_now[0].split("@")[0], cached)
             return torch.nn.functional.normalize(m.embed(x).float(), dim=-1)
 
     var_now = [""]
@@ -64,6 +65,8 @@ def main():
             try:
                 if var.startswith("sdpa="):
                     ctx = sdpa_kernel([backends[var[5:]]])
+                elif "@" in var:                          # model variant @ SDPA backend
+                    ctx = sdpa_kernel([backends[var.split("@")[1]]])
                 else:
                     import contextlib
                     ctx = contextlib.nullcontext()

@@ -5,11 +5,17 @@ set -u
 export PYTHONPATH=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-ds}; mkdir -p $OUT
+if [ -n "${PYTEST_SEL:-}" ]; then
+timeout -k 10 600 python -u -m pytest $PYTEST_SEL -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+fi
+if [ -z "${SKIP_PROBE:-}" ]; then
 timeout -k 10 300 python tools/dreamsim_probe.py 512 > $OUT/probe.jsonl 2> $OUT/probe.err || { tail $OUT/probe.err; exit 1; }
 cat $OUT/probe.jsonl
-timeout -k 10 300 python tools/dreamsim_variants.py --batches 512 --variants ${VARIANTS:-fused,fused_gelu_lt,base} --iters 6 > $OUT/variants.jsonl 2> $OUT/variants.err || { tail $OUT/variants.err; exit 2; }
+fi
+timeout -k 10 300 python tools/dreamsim_variants.py --batches 512 --variants ${VARIANTS:-fused,fused_gelu_lt,fused_gelu_lt@efficient} --iters 6 > $OUT/variants.jsonl 2> $OUT/variants.err || { tail $OUT/variants.err; exit 2; }
 cat $OUT/variants.jsonl
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 tools/dreamsim_variants.py --batches 512 --variants fused --iters 4 > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 3; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 tools/dreamsim_variants.py --batches 512 --variants fused_gelu_lt --iters 4 > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 3; }
 python3 - $OUT/prof/run_kernel_stats.csv <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
