@@ -442,7 +442,8 @@ def main():
                 "workload": cfg["name"], "rows": cfg["rows"], "dim": D_total, "k": a.k,
                 "queries_per_batch": a.nq, "metric": cfg["ranking"],
                 "rows_per_gpu": n_local, "parallelism": (f"query-slice x{qgroups} * row-shard x{world // qgroups}" if qgroups > 1
-                                else f"row-shard x{world}") + " + RCCL all-gather merge",
+                                else f"row-shard x{world}") + (" + RCCL all-gather merge" if backend == "nccl"
+                                                               else f" + {backend} all-gather merge (rehearsal)"),
                 "queries_per_gpu": nq_local,
                 "tile_rows": tr.value, "tile_queries": tq.value, "row_splits": sp.value,
                 "workgroups": wg.value,
