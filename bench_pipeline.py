@@ -8,12 +8,13 @@ reference runs per image:
   colour    HIP histogram kernel (csrc/color_hist.hip; reference vector_scripts/
             create_color_vector.py:18-52: 16 bins per RGB channel, L2-normalised, 48-d)
   dreamsim  resize 256 -> 224 (bicubic, antialiased: the reference resizes with PIL LANCZOS on
-            the CPU) + the DreamSim-architecture ensemble (3 ViT-B/16, 1792-d) on PyTorch-ROCm,
-            bf16 autocast, RANDOM weights (the pretrained weights cannot be downloaded here:
-            throughput only)
+            the CPU) + the DreamSim-architecture ensemble (3 ViT-B/16, 1792-d) on PyTorch-ROCm:
+            bf16 GEMMs from weights cast once, fp32 LayerNorm / residual stream, the fused HIP
+            passes of include/imgrec_vit.h; RANDOM weights (the pretrained weights cannot be
+            downloaded here: throughput only)
   index     concatenate [colour 48 | dreamsim 1792] = 1840-d rows (the SIFT part needs the
             reference's trained VLAD codebook, which is not in the repo) and add them to the
-            resident exact index (HBM copy, norms, split-bf16 copy)
+            resident exact index (HBM copy, norms, bf16 copy)
   search    1024 queries (normalised concatenations of the first 1024 images, as
             main/search_from_image.py:305-322 builds them), k = 10
 
@@ -80,10 +81,25 @@ def run(a) -> dict | None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # IMGREC_DIST_BACKEND=gloo rehearses the N-rank protocol with every rank on one visible GPU
+    # (as bench.py); the measured runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("IMGREC_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if world > 1 and backend == "nccl" and (ndev < world or local >= ndev):
+        raise SystemExit(f"[bench_pipeline] rank {rank}: WORLD_SIZE={world} ranks need {world} "
+                         f"visible GPUs, this process sees {ndev}")
+    if backend != "nccl":
+        local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        from datetime import timedelta
+        tmo = timedelta(seconds=float(os.environ.get("IMGREC_DIST_TIMEOUT_S", "300")))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device, timeout=tmo)
+        else:
+            dist.init_process_group(backend, timeout=tmo)
+        dist.barrier()
 
     from image_recommender_amd.faiss_compat import METRIC_L2
     from image_recommender_amd.sharded import ShardedIndex, shard_range

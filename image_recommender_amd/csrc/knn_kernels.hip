@@ -760,7 +760,9 @@ cert_tail_kernel(const TailArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lane0_acquire();                    // this CU's L1 holds no stale copy of fq either
         }
+        __syncthreads();
     } else {
         if (t == 0) {
             // the planner is running (it completed an item or took ticket 0); the bound only
@@ -1035,16 +1037,21 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
     }
 }
 
-// Second level of the two-level merge (round 3): one 256-thread block per query takes the G <= 64
-// first-level outputs (sorted (key, global label) lists of kin <= 64 entries + G floors), packs
-// them as (order-preserving key bits | local row) u64 in registers (<= 16 per thread), and finds
-// the K = min(kout, valid) smallest by the same bit-by-bit threshold select as the first level,
-// with block-wide counts (32 steps over the key bits; the row bits only when the K-th key is
-// tied).  The K winners are compacted by a block scan and each placed at its rank.  Replaces a
-// one-wave LDS-queue merge (kout rounds of a wave minimum, each behind a dependent LDS read):
-// 32.5 us per query at nq = 1 (profiles/r03/).
-constexpr int kMergeBlockThreads = 256, kMergeBlockPer = 16;    // <= 4096 entries per query
-
+// Block-wide candidate merge (round 3), one NT-thread block per query: the query's M = nlists x kin
+// entries (sorted (key, global label) lists, label -1 = empty, at cd / ci + q * stride_q, list l
+// at l * kin) are packed as (order-preserving key bits | local row) u64 in registers (PER per
+// thread) and the K = min(kout, valid) smallest are found by the same bit-by-bit threshold select
+// as cand_merge_lane_kernel, with block-wide counts: 32 steps over the key bits — fewer, from
+// the highest bit where the smallest and largest valid value differ — and the row bits only when
+// the K-th key is tied.  The K winners are compacted by a block scan and each placed at its rank.
+// Floor = min(floor_in of every list, when given; the last key of every full list).
+// Used as the second level after cand_merge_lane_kernel (NT 256, G <= 64 lists of <= 64), where
+// it replaced a one-wave LDS-queue merge (32.5 -> 17.3 us per query at nq = 1).  Measured and
+// dropped: the whole merge of a small batch in one 1024-thread block per query (2048 lists x 16
+// at nq = 1, 32 entries per thread): 50.1 us against the two levels' 32 us — one CU's VALU
+// issue of the counts, where level 1 spreads the lists over 32 waves on as many CUs
+// (profiles/r03/nq1_single_level_merge_rejected.csv).
+template <int NT>
 __device__ __forceinline__ int block_sum_i32(int x, int* red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int w = wave_sum_i32(x);
@@ -1052,35 +1059,39 @@ __device__ __forceinline__ int block_sum_i32(int x, int* red) {
     __syncthreads();
     int tot = 0;
 #pragma unroll
-    for (int i = 0; i < kMergeBlockThreads / 64; ++i) tot += red[i];
+    for (int i = 0; i < NT / 64; ++i) tot += red[i];
     __syncthreads();                                  // red reused by the next call
     return tot;
 }
 
-__global__ void __launch_bounds__(kMergeBlockThreads)
+template <int NT, int PER>
+__global__ void __launch_bounds__(NT)
 cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int64_t nq,
-                        int nlists, int kin, int kout, int64_t id_offset,
+                        int nlists, int kin, int64_t stride_q, int kout, int64_t id_offset,
                         const float* __restrict__ floor_in, float* __restrict__ D,
                         int64_t* __restrict__ I, float* __restrict__ floor_out) {
-    __shared__ int red[kMergeBlockThreads / 64];
-    __shared__ float redf[kMergeBlockThreads / 64];
+    constexpr int NW = NT / 64;
+    __shared__ int red[NW];
+    __shared__ float redf[NW];
+    __shared__ uint64_t redm[2][NW];
     __shared__ uint64_t sel[64];
     constexpr uint64_t kEmpty = ~0ull;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int64_t q = blockIdx.x;
     const int M = nlists * kin;
-    __shared__ uint64_t redm[2][kMergeBlockThreads / 64];
-    uint64_t v[kMergeBlockPer];
+    const float* qd = cd + q * stride_q;
+    const int64_t* qi = ci + q * stride_q;
+    uint64_t v[PER];
     int nvl = 0;
     uint64_t vmin = kEmpty, vmax = 0;
 #pragma unroll
-    for (int j = 0; j < kMergeBlockPer; ++j) {
-        const int e = t + j * kMergeBlockThreads;
+    for (int j = 0; j < PER; ++j) {
+        const int e = t + j * NT;
         v[j] = kEmpty;
         if (e < M) {
-            const int64_t lab = ci[q * M + e];
+            const int64_t lab = qi[e];
             if (lab >= 0) {
-                v[j] = ((uint64_t)key_bits_ordered(cd[q * M + e]) << 32) | (uint32_t)(lab - id_offset);
+                v[j] = ((uint64_t)key_bits_ordered(qd[e]) << 32) | (uint32_t)(lab - id_offset);
                 ++nvl;
                 vmin = v[j] < vmin ? v[j] : vmin;
                 vmax = v[j] > vmax ? v[j] : vmax;
@@ -1090,12 +1101,11 @@ cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict_
     vmin = wave_min_u64(vmin);
     vmax = ~wave_min_u64(~vmax);
     if (lane == 0) { redm[0][wave] = vmin; redm[1][wave] = vmax; }
-    // floor: the first level's floors and the last key of every full first-level list
     float fl = INFINITY;
-    if (t < nlists) {
-        fl = floor_in[q * nlists + t];
-        const int64_t last = (q * nlists + t) * kin + kin - 1;
-        if (ci[last] >= 0) fl = fminf(fl, cd[last]);
+    for (int l = t; l < nlists; l += NT) {
+        if (floor_in) fl = fminf(fl, floor_in[q * nlists + l]);
+        const int last = l * kin + kin - 1;
+        if (qi[last] >= 0) fl = fminf(fl, qd[last]);       // a full list: its last key
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
@@ -1103,20 +1113,20 @@ cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict_
     auto count_le = [&](uint64_t x) __attribute__((always_inline)) {
         int c = 0;
 #pragma unroll
-        for (int j = 0; j < kMergeBlockPer; ++j) c += v[j] <= x ? 1 : 0;
+        for (int j = 0; j < PER; ++j) c += v[j] <= x ? 1 : 0;
         return c;
     };
-    const int K = min(kout, block_sum_i32(nvl, red));   // (its barrier also publishes redf)
+    const int K = min(kout, block_sum_i32<NT>(nvl, red));   // (its barrier publishes redf, redm)
     if (t == 0) {
         float f = redf[0];
 #pragma unroll
-        for (int i = 1; i < kMergeBlockThreads / 64; ++i) f = fminf(f, redf[i]);
+        for (int i = 1; i < NW; ++i) f = fminf(f, redf[i]);
         floor_out[q] = f;
     }
     uint64_t T = 0;
     if (K > 0) {
         // bits above the highest difference of the valid values' min and max are common to T
-        for (int i = 0; i < kMergeBlockThreads / 64; ++i) {
+        for (int i = 0; i < NW; ++i) {
             vmin = redm[0][i] < vmin ? redm[0][i] : vmin;
             vmax = redm[1][i] > vmax ? redm[1][i] : vmax;
         }
@@ -1124,13 +1134,13 @@ cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict_
         uint64_t prefix = hb < 0 ? vmin : (hb >= 63 ? 0 : vmin & ~((2ull << hb) - 1));
         for (int b = min(hb, 63); b >= 32; --b) {
             const uint64_t lo = prefix | ((1ull << b) - 1);
-            if (block_sum_i32(count_le(lo), red) < K) prefix |= 1ull << b;
+            if (block_sum_i32<NT>(count_le(lo), red) < K) prefix |= 1ull << b;
         }
         T = prefix | 0xffffffffull;
-        if (block_sum_i32(count_le(T), red) > K) {        // the K-th key is tied: rows decide
+        if (block_sum_i32<NT>(count_le(T), red) > K) {    // the K-th key is tied: rows decide
             for (int b = min(hb, 31); b >= 0; --b) {
                 const uint64_t lo = prefix | ((1ull << b) - 1);
-                if (block_sum_i32(count_le(lo), red) < K) prefix |= 1ull << b;
+                if (block_sum_i32<NT>(count_le(lo), red) < K) prefix |= 1ull << b;
             }
             T = prefix;
         }
@@ -1143,7 +1153,7 @@ cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict_
     int base = wex;
     for (int i = 0; i < wave; ++i) base += red[i];
 #pragma unroll
-    for (int j = 0; j < kMergeBlockPer; ++j)
+    for (int j = 0; j < PER; ++j)
         if (v[j] <= T && K > 0) sel[base++] = v[j];
     __syncthreads();
     if (t < K) {
@@ -1192,8 +1202,9 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
         // (32.3 us), and a 256-thread rank form (binary searches of every entry in every other
         // queue, 123 us: dependent LDS reads per thread).
 #undef IMGREC_CAND_LANE
-        hipLaunchKernelGGL(cand_merge_block_kernel, dim3((unsigned)nq), dim3(kMergeBlockThreads), 0, st,
-                           ws_d, ws_i, nq, G, kout, kout, id_offset, ws_floor, D, I, floor);
+        hipLaunchKernelGGL((cand_merge_block_kernel<256, 16>), dim3((unsigned)nq), dim3(256), 0, st,
+                           ws_d, ws_i, nq, G, kout, (int64_t)G * kout, kout, id_offset, ws_floor, D, I,
+                           floor);
         return hipGetLastError();
     }
     // one wave per query; the lane lists hold 16 entries (what a lane drops beyond that is

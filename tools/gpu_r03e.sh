@@ -19,3 +19,5 @@ for r in 500000 250000; do timeout -k 10 200 python bench.py --rows $r --profile
 cat $OUT/shards.jsonl
 timeout -k 10 400 python bench_pipeline.py --images 20000 > $OUT/pipeline_20k.json 2> $OUT/pipeline_20k.err || { tail $OUT/pipeline_20k.err; exit 5; }
 cut -c1-700 $OUT/pipeline_20k.json
+IMGREC_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench_pipeline.py --gpus 2 --images 4096 --model-batch 256 --nq 256 --search-reps 2 > $OUT/pipeline_gloo_n2.json 2> $OUT/pipeline_gloo_n2.err || { tail -20 $OUT/pipeline_gloo_n2.err; exit 6; }
+cut -c1-600 $OUT/pipeline_gloo_n2.json
