@@ -150,6 +150,29 @@ def _tokens(pe, cls, pos):
     return out
 
 
+def _attn(qkv, heads):
+    """Self-attention of every (image, head) from the qkv Linear's output (B, N, 3 * C) bf16 ->
+    (B, N, C) bf16 in one HIP kernel (vit_attention_bf16): no q / k / v permute copies, no output
+    transpose, the 197-token rows unpadded."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    b, n, c3 = qkv.shape
+    c = c3 // 3
+    hd = c // heads
+    qkv = qkv.contiguous()
+    if qkv.dtype != torch.bfloat16 or not qkv.is_cuda:
+        raise TypeError("_attn: qkv must be a bf16 GPU tensor")
+    out = torch.empty((b, n, c), dtype=torch.bfloat16, device=qkv.device)
+    rc = _lib.load().vit_attention_bf16(C.c_void_p(qkv.data_ptr()), b, n, heads, hd,
+                                        C.c_float(1.0 / math.sqrt(hd)), C.c_void_p(out.data_ptr()),
+                                        C.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_attention_bf16 failed")
+    return out
+
+
 def _gelu_(h):
     """nn.GELU (erf form) in place on a contiguous bf16 tensor (vit_gelu_bf16)."""
     import ctypes as C
@@ -205,10 +228,13 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             """The same block on the fused kernels: x (fp32 residual, updated in place) first takes
             the previous block's bf16 output `delta`; returns this block's bf16 output."""
             b, n, c = x.shape
-            qkv = _lin(self.qkv, _add_ln(x, delta, self.ln1)).view(b, n, 3, self.heads, c // self.heads)
-            q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)
-            a = F.scaled_dot_product_attention(q, k, v)
-            y = _add_ln(x, _lin(self.proj, a.transpose(1, 2).reshape(b, n, c)), self.ln2)
+            qkv = _lin(self.qkv, _add_ln(x, delta, self.ln1))
+            if getattr(self, "hip_attn", False):
+                a = _attn(qkv, self.heads)
+            else:
+                q, k, v = qkv.view(b, n, 3, self.heads, c // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
+                a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(b, n, c)
+            y = _add_ln(x, _lin(self.proj, a), self.ln2)
             if self.quick_gelu:
                 h = _quick_gelu_(_lin(self.fc1, y))
             elif getattr(self, "gelu_epilogue", False):
@@ -282,16 +308,19 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             parts = [F.normalize(t(x).float(), dim=-1) for t in self.towers]
             return torch.cat(parts, -1)
 
-        def prepare_inference(self, dtype, fused=False, gelu_epilogue=False):
+        def prepare_inference(self, dtype, fused=False, gelu_epilogue=False, hip_attn=None):
             """Cache low-precision copies of every matrix-product weight once (autocast would
             re-cast them on every forward); LayerNorms and the residual stream stay fp32.
             fused (bf16, on a GPU): residual add + LayerNorm + bf16 cast and QuickGELU run as
             single HIP passes (include/imgrec_vit.h).  gelu_epilogue (with fused): the erf
-            GELU after fc1 becomes the GEMM's own epilogue (_lin_gelu)."""
+            GELU after fc1 becomes the GEMM's own epilogue (_lin_gelu).  hip_attn (with fused;
+            default on): attention through the one-kernel vit_attention_bf16 (_attn) instead of
+            torch SDPA."""
             for t in self.towers:
                 t.fused = bool(fused) and dtype == torch.bfloat16
                 for blk in t.blocks:
                     blk.gelu_epilogue = t.fused and bool(gelu_epilogue)
+                    blk.hip_attn = t.fused and (hip_attn is None or bool(hip_attn))
             for m in self.modules():
                 if isinstance(m, (nn.Linear, nn.Conv2d)):
                     w = m.weight.detach()

@@ -42,6 +42,15 @@ int vit_patchify_bf16(const float* img, int64_t batch, int height, int width, in
 int vit_tokens_f32(const uint16_t* patch_emb, const float* cls, const float* pos, int64_t batch,
                    int npatch, int dim, float* out, void* stream);
 
+/* Multi-head self-attention softmax(q k^T * scale) v of every (image, head), without masks
+ * (torch.nn.functional.scaled_dot_product_attention with scale = 1/sqrt(head_dim)): qkv is the
+ * qkv Linear's output (batch, ntok, 3, heads, head_dim) bf16, out (batch, ntok, heads * head_dim)
+ * bf16 (the output projection's input layout).  head_dim = 64, ntok <= 256; scores, softmax and
+ * the output accumulate in fp32 (bf16 probabilities into the P.V products); 16-B aligned
+ * pointers (csrc/vit_attn.hip). */
+int vit_attention_bf16(const uint16_t* qkv, int64_t batch, int ntok, int heads, int head_dim,
+                       float scale, uint16_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -104,3 +104,49 @@ def test_patchify_and_tokens_match_torch(gpu):
     tok = _tokens(pe, cls, pos)
     torch.cuda.synchronize()
     assert torch.equal(tok, torch.cat([cls.expand(3, -1, -1), pe.float()], 1) + pos)
+
+
+@pytest.mark.parametrize("b,n,heads", [(3, 197, 12), (2, 16, 2), (1, 1, 1), (2, 50, 3), (1, 256, 4),
+                                       (4, 33, 12), (2, 208, 1), (1, 17, 5)])
+def test_attention_matches_torch(gpu, b, n, heads):
+    """vit_attention_bf16 against torch's fp32 SDPA on the same bf16 q / k / v: within the bf16
+    rounding of the probabilities (the P.V products take bf16 P) and of the output."""
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import _attn
+    g = torch.Generator(device="cuda").manual_seed(b * 1000 + n * 10 + heads)
+    qkv = (torch.randn(b, n, 3 * heads * 64, device="cuda", generator=g) * 1.5).bfloat16()
+    q, k, v = qkv.float().view(b, n, 3, heads, 64).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = torch.nn.functional.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(b, n, heads * 64)
+    out = _attn(qkv, heads)
+    torch.cuda.synchronize()
+    err = (out.float() - ref).abs()
+    # |P_bf16 - P| <= 2^-9 P per entry, so |sum (P_bf16 - P) v| <= 2^-9 max|v|; plus the output's
+    # own bf16 rounding
+    vmax = v.abs().amax(dim=(-2, -1))                    # (b, heads)
+    bound = 2.0 ** -8 * ref.abs() + 2.0 ** -8 * vmax.repeat_interleave(64, dim=1)[:, None, :] + 1e-5
+    assert float((err - bound).max()) <= 0.0, float(err.max())
+
+
+def test_attention_rejects_bad_shapes(gpu):
+    import ctypes as C
+    from image_recommender_amd import _lib
+    qkv = torch.zeros(1, 300, 3 * 64, dtype=torch.bfloat16, device="cuda")
+    out = torch.zeros(1, 300, 64, dtype=torch.bfloat16, device="cuda")
+    lib = _lib.load()
+    assert lib.vit_attention_bf16(C.c_void_p(qkv.data_ptr()), 1, 300, 1, 64, C.c_float(0.125),
+                                  C.c_void_p(out.data_ptr()), None) == -1          # ntok > 256
+    assert lib.vit_attention_bf16(C.c_void_p(qkv.data_ptr()), 1, 100, 1, 32, C.c_float(0.125),
+                                  C.c_void_p(out.data_ptr()), None) == -1          # head_dim != 64
+
+
+def test_fused_forward_hip_attention_matches_sdpa(gpu):
+    """The fused forward with the HIP attention against the same forward on torch SDPA."""
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import build_ensemble
+    x = torch.rand((4, 3, 224, 224), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    sdpa = build_ensemble(seed=0, depth=4).cuda().eval().prepare_inference(torch.bfloat16, fused=True,
+                                                                           hip_attn=False)
+    hip = build_ensemble(seed=0, depth=4).cuda().eval().prepare_inference(torch.bfloat16, fused=True)
+    with torch.no_grad():
+        a = sdpa.embed(x).float()
+        c = hip.embed(x).float()
+    cos = (torch.nn.functional.normalize(a, dim=-1) * torch.nn.functional.normalize(c, dim=-1)).sum(-1)
+    assert float(cos.min()) > 0.999, cos

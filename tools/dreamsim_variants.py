@@ -11,6 +11,8 @@ images/s of variants on one GPU, random weights, bf16 autocast, 224 x 224 inputs
   fused      residual add + LayerNorm + bf16 cast and QuickGELU as single HIP passes
              (include/imgrec_vit.h)
   fused_gelu_lt  fused + fc1's GELU as the hipBLASLt GELU_BIAS epilogue (torch._addmm_activation)
+             + attention as one HIP kernel (vit_attention_bf16, the default since round 3)
+  fused_gelu_lt_sdpa  the same with attention on torch SDPA (round 3's earlier form)
   X@B        variant X with SDPA restricted to backend B (flash / efficient / math)
 
 FLOP per image: 3 ViT-B/16 towers at 224 (197 tokens): 2 x 17.58 GMAC each -> 105.5 GFLOP;
@@ -43,16 +45,20 @@ def main():
     dev = torch.device("cuda", 0)
     model = build_ensemble(seed=0).to(dev).eval()
     cached = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16)
-    fused = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True)
+    fused = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True,
+                                                                   hip_attn=False)
     fused_lt = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True,
                                                                       gelu_epilogue=True)
+    fused_lt_sdpa = build_ensemble(seed=0).to(dev).eval().prepare_inference(
+        torch.bfloat16, fused=True, gelu_epilogue=True, hip_attn=False)
 
     def embed(x):
         if var_now[0].startswith("autocast"):        # per-call weight casts (the r01 form)
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
                 return torch.nn.functional.normalize(model.embed(x).float(), dim=-1)
         with torch.no_grad():                          # weights cast once (the shipped form)
-            m = {"fused": fused, "fused_gelu_lt": fused_lt}.get(var_now[0].split("@")[0], cached)
+            m = {"fused": fused, "fused_gelu_lt": fused_lt,
+                 "fused_gelu_lt_sdpa": fused_lt_sdpa}.get(var_now[0].split("@")[0], cached)
             return torch.nn.functional.normalize(m.embed(x).float(), dim=-1)
 
     var_now = [""]
