@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--single-query-steps", type=int, default=50)
-    ap.add_argument("--mode", choices=("auto", "exact", "split", "bf16"), default="auto",
+    ap.add_argument("--mode", choices=("auto", "exact", "split", "bf16", "i8"), default="auto",
                     help="search arithmetic (include/imgrec_knn.h knn_search_mode)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed steps (for rocprofv3 runs)")
@@ -354,7 +354,7 @@ def main():
     torch.cuda.synchronize()
     elapsed, _, (Dr, Ir) = region(step, a.steps, False)          # the bench value
     split_q, fallback_q, err_ratio = shard.index.search_stats(with_error=True)   # last step
-    path = lib.knn_last_path(h)                                # 0 exact, 1 split, 2 bf16
+    path = lib.knn_last_path(h)                                # 0 exact, 1 split, 2 bf16, 3 i8
     kel, kern_ms, _ = region(step, a.steps, True)               # candidate-kernel duration
     if a.profile_only:
         if rank == 0:
@@ -383,7 +383,7 @@ def main():
     torch.cuda.synchronize()
     el1, _, _ = region(lambda: shard.search(q1, a.k), a.single_query_steps, False)
     _, kern1_ms, _ = region(lambda: shard.search(q1, a.k), a.single_query_steps, True)
-    path1 = lib.knn_last_path(h)                               # 0 exact, 1 split, 2 bf16
+    path1 = lib.knn_last_path(h)                               # 0 exact, 1 split, 2 bf16, 3 i8
 
     tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
     lib.knn_plan(shard.index.handle, nq_local, a.k, C.byref(tr), C.byref(tq), C.byref(sp), C.byref(wg))
@@ -416,9 +416,11 @@ def main():
                  1: "bf16x3 split (fp32-equivalent) + fp32 rerank"}.get(path, "fp32")
         bytes1 = 4.0 * n_local * D_total + 4.0 * n_local    # the fp32 corpus + norms (algorithmic)
         dpb = (D_total + 63) // 64 * 64
-        # what the single-query kernel actually streams: the bf16 copy (bf16 path), the split copy
-        # (hi + lo, as much as fp32) or the fp32 rows
-        stream1 = (2.0 * n_local * dpb if path1 == 2 else 4.0 * n_local * D_total) + 4.0 * n_local
+        # what the single-query kernel actually streams: the int8 copy (codes + one fp32 scale per
+        # 64 elements), the bf16 copy (bf16 path), the split copy (hi + lo, as much as fp32) or
+        # the fp32 rows
+        stream1 = ({3: 1.0 * n_local * dpb + 4.0 * n_local * (dpb // 64), 2: 2.0 * n_local * dpb}
+                   .get(path1, 4.0 * n_local * D_total) + 4.0 * n_local)
         busy = pmc_record(kpat, "_clock.json") if default_run else None
         qps = a.nq * a.steps / elapsed
         out = {
@@ -469,7 +471,7 @@ def main():
             "single_query": {
                 "queries_per_s": a.single_query_steps / el1,
                 "kernel_ms": kern1_ms,
-                "path": {0: "exact", 1: "split", 2: "bf16"}.get(path1, "?"),
+                "path": {0: "exact", 1: "split", 2: "bf16", 3: "i8"}.get(path1, "?"),
                 "hbm_gbs": stream1 / (kern1_ms * 1e-3) / 1e9,
                 "hbm_frac": stream1 / (kern1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "fp32_equivalent_gbs": bytes1 / (kern1_ms * 1e-3) / 1e9,

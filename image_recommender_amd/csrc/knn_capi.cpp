@@ -67,8 +67,12 @@ int reserve_rows(knn_index* ix, int64_t need, hipStream_t st) {
     uint32_t* nxs = nullptr;
     uint16_t* nxh = nullptr;
     float* nxr = nullptr;
+    int8_t* nx8 = nullptr;
+    float* nx8s = nullptr;
+    float* nx8r = nullptr;
     auto release = [&]() {
-        for (void* p : {(void*)nxb, (void*)nxn, (void*)nxs, (void*)nxh, (void*)nxr})
+        for (void* p : {(void*)nxb, (void*)nxn, (void*)nxs, (void*)nxh, (void*)nxr, (void*)nx8,
+                        (void*)nx8s, (void*)nx8r})
             if (p) (void)hipFree(p);
     };
     hipError_t e = hipMalloc((void**)&nxb, (size_t)ncap * ix->dp * sizeof(float));
@@ -77,6 +81,11 @@ int reserve_rows(knn_index* ix, int64_t need, hipStream_t st) {
     if (e == hipSuccess && ix->xs) e = hipMalloc((void**)&nxs, (size_t)ncap * ix->dp * sizeof(uint32_t));
     if (e == hipSuccess && ix->b16_ok) e = hipMalloc((void**)&nxh, (size_t)ncap * ix->dpb * sizeof(uint16_t));
     if (e == hipSuccess && ix->b16_ok) e = hipMalloc((void**)&nxr, (size_t)ncap * sizeof(float));
+    // the int8 copy exists only once a small-batch search has materialised it (ensure_i8)
+    const size_t row8 = (size_t)i8_row_bytes(ix->nblk8);
+    if (e == hipSuccess && ix->x8) e = hipMalloc((void**)&nx8, (size_t)ncap * row8);
+    if (e == hipSuccess && ix->x8) e = hipMalloc((void**)&nx8s, (size_t)ncap * ix->nblk8 * sizeof(float));
+    if (e == hipSuccess && ix->x8) e = hipMalloc((void**)&nx8r, (size_t)ncap * sizeof(float));
     if (e != hipSuccess) {
         release();
         (void)hipGetLastError();
@@ -95,14 +104,21 @@ int reserve_rows(knn_index* ix, int64_t need, hipStream_t st) {
     if (e == hipSuccess && nxs) e = copy_tail(nxs, ix->xs, (size_t)ix->dp * sizeof(uint32_t), (size_t)ncap);
     if (e == hipSuccess && nxh) e = copy_tail(nxh, ix->xh, (size_t)ix->dpb * sizeof(uint16_t), (size_t)ncap);
     if (e == hipSuccess && nxr) e = copy_tail(nxr, ix->xr, sizeof(float), (size_t)ncap);
+    if (e == hipSuccess && nx8) e = copy_tail(nx8, ix->x8, row8, (size_t)ncap);
+    if (e == hipSuccess && nx8s) e = copy_tail(nx8s, ix->x8s, (size_t)ix->nblk8 * sizeof(float), (size_t)ncap);
+    if (e == hipSuccess && nx8r) e = copy_tail(nx8r, ix->x8r, sizeof(float), (size_t)ncap);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         (void)hipStreamSynchronize(st);
         release();
         KNN_FAIL(KNN_EHIP, "corpus regrowth failed: %s", hipGetErrorString(e));
     }
-    for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xh, (void*)ix->xr})
+    for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xh, (void*)ix->xr,
+                    (void*)ix->x8, (void*)ix->x8s, (void*)ix->x8r})
         if (p) (void)hipFree(p);
+    ix->x8 = nx8;
+    ix->x8s = nx8s;
+    ix->x8r = nx8r;
     ix->xb = nxb;
     ix->xn = nxn;
     ix->xs = nxs;
@@ -125,6 +141,10 @@ int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st) 
     if (ix->b16_ok)
         KNN_HIP(launch_bf16_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp, ix->dpb,
                                  ix->xh + (size_t)ix->ntotal * ix->dpb, ix->xr + ix->ntotal, st));
+    if (ix->x8)
+        KNN_HIP(launch_i8_rows(ix->xb + (size_t)ix->ntotal * ix->dp, n, ix->dp, ix->nblk8,
+                               ix->x8 + (size_t)ix->ntotal * i8_row_bytes(ix->nblk8),
+                               ix->x8s + (size_t)ix->ntotal * ix->nblk8, ix->x8r + ix->ntotal, st));
     ix->ntotal += n;
     ix->xn_max_stale = true;
     return KNN_OK;
@@ -148,6 +168,34 @@ int ensure_split(knn_index* ix, hipStream_t st) {
     return KNN_OK;
 }
 
+// The block-scaled int8 copy (i8_row_bytes(nblk8) + nblk8 scales + one residual per row, about half
+// the bf16 copy) is built on the first search that runs the int8 small-batch path, from the stored
+// fp32 rows, and kept up to date by later adds (the split copy's pattern).
+int ensure_i8(knn_index* ix, hipStream_t st) {
+    if (ix->x8) return KNN_OK;
+    if (ix->nblk8 <= 0) KNN_FAIL(KNN_EINVAL, "int8 search needs 64 <= d <= 4096; d = %d", ix->d);
+    const size_t cap = (size_t)std::max<int64_t>(ix->cap, 1);
+    int8_t* x8 = nullptr;
+    float* x8s = nullptr;
+    float* x8r = nullptr;
+    hipError_t e = hipMalloc((void**)&x8, cap * (size_t)i8_row_bytes(ix->nblk8));
+    if (e == hipSuccess) e = hipMalloc((void**)&x8s, cap * ix->nblk8 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc((void**)&x8r, cap * sizeof(float));
+    if (e != hipSuccess) {
+        for (void* p : {(void*)x8, (void*)x8s, (void*)x8r})
+            if (p) (void)hipFree(p);
+        (void)hipGetLastError();
+        KNN_FAIL(KNN_ENOMEM, "hipMalloc of the %lld-row int8 copy failed", (long long)ix->cap);
+    }
+    ix->x8 = x8;
+    ix->x8s = x8s;
+    ix->x8r = x8r;
+    ix->xn_max_stale = true;             // refresh_maxima computes the int8 residual maximum
+    if (ix->ntotal > 0)
+        KNN_HIP(launch_i8_rows(ix->xb, ix->ntotal, ix->dp, ix->nblk8, ix->x8, ix->x8s, ix->x8r, st));
+    return KNN_OK;
+}
+
 int create_single(int d, int metric, int device, knn_index** out) {
     *out = nullptr;
     int ndev = 0;
@@ -166,6 +214,7 @@ int create_single(int d, int metric, int device, knn_index** out) {
     ix->split_ok = ix->dp % 32 == 0 && d >= 256;
     ix->b16_ok = d >= 64;
     ix->dpb = (int)round_up(d, kB16Pad);
+    ix->nblk8 = d >= 64 && d <= 4096 ? (d + 63) / 64 : 0;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
@@ -183,6 +232,8 @@ int create_single(int d, int metric, int device, knn_index** out) {
 void free_single(knn_index* ix) {
     DeviceGuard g(ix->device);
     (void)hipDeviceSynchronize();       // searches on other streams may still use the buffers
+    for (void* p : {(void*)ix->x8, (void*)ix->x8s, (void*)ix->x8r, (void*)ix->x8r_max})
+        if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xh, (void*)ix->xr, (void*)ix->xr_max, (void*)ix->qb16,
                     (void*)ix->q_resid, (void*)ix->floor, (void*)ix->mws_d, (void*)ix->mws_i,
                     (void*)ix->mws_f, (void*)ix->stat, (void*)ix->fb_cd, (void*)ix->fb_ci,
@@ -455,7 +506,7 @@ int knn_kernel_time(knn_index_t* ix, double* total_ms, int* launches) {
 int knn_set_search_mode(knn_index_t* ix, int mode) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
     if (mode != KNN_SEARCH_AUTO && mode != KNN_SEARCH_EXACT && mode != KNN_SEARCH_SPLIT &&
-        mode != KNN_SEARCH_BF16)
+        mode != KNN_SEARCH_BF16 && mode != KNN_SEARCH_I8)
         KNN_FAIL(KNN_EINVAL, "unknown search mode %d", mode);
     if (ix->multi) return multi_set_search_mode(ix, mode);
     std::lock_guard<std::mutex> lk(ix->mu);
@@ -463,6 +514,8 @@ int knn_set_search_mode(knn_index_t* ix, int mode) {
         KNN_FAIL(KNN_EINVAL, "split search needs d >= 256; d = %d", ix->d);
     if (mode == KNN_SEARCH_BF16 && !ix->b16_ok)
         KNN_FAIL(KNN_EINVAL, "bf16 search needs d >= 64; d = %d", ix->d);
+    if (mode == KNN_SEARCH_I8 && ix->nblk8 <= 0)
+        KNN_FAIL(KNN_EINVAL, "int8 search needs 64 <= d <= 4096; d = %d", ix->d);
     ix->mode = mode;
     return KNN_OK;
 }
@@ -495,7 +548,8 @@ int knn_plan(const knn_index_t* cix, int64_t nq, int k, int* tr, int* tq, int* s
     if (!cix || !tr || !tq || !splits || !wgs) KNN_FAIL(KNN_EINVAL, "NULL argument");
     const knn_index* ix = cix->multi ? multi_shard(cix, 0) : cix;
     const int64_t cn = std::min(nq, kQueryChunk);
-    const Plan p = use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
+    const Plan p = use_i8(ix, cn, k) ? make_i8_plan(ix->ntotal, cn, k, ix->cus)
+                 : use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                  : use_split(ix, cn, k) ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                                         : make_plan(ix->ntotal, cn, k, ix->cus);
     *tr = p.bm;
@@ -510,7 +564,11 @@ int knn_plan_kernel(const knn_index_t* cix, int64_t nq, int k, char* name, int c
     const knn_index* ix = cix->multi ? multi_shard(cix, 0) : cix;
     const int64_t cn = std::min(nq, kQueryChunk);
     const int l2 = ix->metric == KNN_METRIC_L2 ? 1 : 0;
-    if (use_b16(ix, cn, k)) {
+    if (use_i8(ix, cn, k)) {
+        const Plan p = make_i8_plan(ix->ntotal, cn, k, ix->cus);
+        std::snprintf(name, cap, "knn_i8_scan_kernel<%d, %d, %d>", cn <= 2 ? (int)cn : 4, p.km,
+                      (ix->nblk8 + 15) / 16);
+    } else if (use_b16(ix, cn, k)) {
         const Plan p = make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb);
         if (p.big && IMGREC_B16_MFMA16)
             std::snprintf(name, cap, "knn_b16w_tile_kernel<%d, %d, %s>", p.km, l2, p.ib > 0 ? "true" : "false");

@@ -1,0 +1,341 @@
+// knn_i8.hip — the small-batch candidate pass on a block-scaled int8 copy of the corpus (gfx950).
+//
+// A search of one or two queries (the reference CLI's regime: main/search_from_image.py:247
+// searches ONE query vector per call) is HBM-bound: the bf16 candidate pass streams 2 bytes per
+// element (3.97 GB at 1M x 1968; 0.646 ms at 6.1 TB/s, profiles/r03/nq1_final.jsonl).  This pass
+// streams 1 byte per element plus one fp32 scale per 64 (2.1 GB) and keeps the same contract as
+// the bf16 pass: per (query, row split) the KM best APPROXIMATE keys, which the candidate merge,
+// the fp32 rerank and the certificate (knn_refine.hip, knn_certify.h kModeI8) turn into the exact
+// answer.  The approximation is certified, not trusted:
+//
+//   x~ = s_b * c   per 64-element block b, s_b = max|x_b| / 127, c = rint(x / s_b) in [-127, 127]
+//   |q.x - q.x~| <= |q| |x - x~| <= |q| R           (R = max stored residual norm)
+//
+// and the query stays fp32 (no query rounding term).  On the bench rows (1M x 1968, unit-norm
+// parts) R = 0.016 against the bf16 copy's 0.0036; the rows within the certificate's band of the
+// 10th approximate key number 21-53 per query (numpy over the whole 1M corpus, DESIGN.md
+// "Small batches"), below the rerank's 64 candidates.
+//
+// Scan: one workgroup per row split (8-row groups s, s + nsplit, ... as the bf16 kernels, so a
+// store with similar images on adjacent rows spreads them over every split), four waves; a wave
+// takes one 8-row group at a time, a 16-lane group per row, lane j the 64-element blocks j,
+// j + 16, ... of its row: 16-B code loads, the query from LDS in fp32, int8 -> fp32 by the SDWA
+// byte-select convert, FMA chains per 16-element chunk, the block scale, a DPP row-rotate sum over
+// the 16 lanes.  Lane j (< NQ) of each group keeps query j's list; at the end the 16 lists of a
+// split are merged in LDS to one list of KM.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "knn_kernels.h"
+
+namespace imgrec {
+namespace {
+
+constexpr int kBlk = 64;       // elements per scale block
+constexpr int kWaves = 4;
+constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA piece)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// sum over the 16 lanes of a DPP row (row_ror 8, 4, 2, 1): every lane gets the row's total
+__device__ __forceinline__ float row16_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+    return v;
+}
+
+// Build: one wave per row, lane b quantises block b (nblk <= 64); rows padded to whole 16-block
+// groups with zero codes (the build zero-fills the slots of blocks >= nblk: see launch_i8_rows).  The residual norm is computed
+// against the dequantised value the scan uses (s * c) and inflated for its own fp32 evaluation.
+__global__ void __launch_bounds__(256)
+i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t* __restrict__ codes,
+               float* __restrict__ scales, float* __restrict__ resid) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const float* x = xb + row * dp;
+    float rsq = 0.f, xsq = 0.f;
+    if (lane < nblk) {
+        float v[kBlk];
+        float mx = 0.f;
+#pragma unroll
+        for (int e = 0; e < kBlk; ++e) {
+            const int i = lane * kBlk + e;
+            v[e] = i < dp ? x[i] : 0.f;
+            mx = fmaxf(mx, fabsf(v[e]));
+        }
+        const float s = mx / 127.f;
+        const float inv = mx > 0.f ? 127.f / mx : 0.f;
+        uint32_t w[kBlk / 4];
+#pragma unroll
+        for (int e4 = 0; e4 < kBlk / 4; ++e4) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float ve = v[4 * e4 + t];
+                const int c = max(-127, min(127, (int)rintf(ve * inv)));
+                const float r = ve - (float)c * s;
+                rsq = fmaf(r, r, rsq);
+                xsq = fmaf(ve, ve, xsq);
+                word |= ((uint32_t)c & 0xffu) << (8 * t);
+            }
+            w[e4] = word;
+        }
+        // chunk c of block b at 16-B slot 16 (4 (b / 16) + c) + b % 16 of the row (i8_row_bytes)
+        uint4* dst = reinterpret_cast<uint4*>(codes + row * (int64_t)i8_row_bytes(nblk)) +
+                     64 * (lane >> 4) + (lane & 15);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dst[16 * c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+        scales[row * nblk + lane] = s;
+    } else if (lane < 16 * ((nblk + 15) / 16)) {      // the padding slots of the last group
+        uint4* dst = reinterpret_cast<uint4*>(codes + row * (int64_t)i8_row_bytes(nblk)) +
+                     64 * (lane >> 4) + (lane & 15);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dst[16 * c] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    rsq = wave_sum(rsq);
+    xsq = wave_sum(xsq);
+    // |fl(c s) - c s| <= 2^-24 |c s| per element: 2^-22 |x| covers the evaluation of every term
+    if (lane == 0) resid[row] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
+}
+
+// Ascending list, labels arriving in increasing order: slot p's key is the median of (kd[p-1], d,
+// kd[p]) (ties keep the earlier, smaller label); d = +inf is a no-op.
+template <int K>
+__device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float d, int id) {
+    bool c[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) c[p] = d < kd[p];
+#pragma unroll
+    for (int p = K - 1; p > 0; --p) {
+        kd[p] = __builtin_amdgcn_fmed3f(kd[p - 1], d, kd[p]);
+        const int nx = c[p] ? id : ki[p];
+        ki[p] = c[p - 1] ? ki[p - 1] : nx;
+    }
+    kd[0] = c[0] ? d : kd[0];
+    ki[0] = c[0] ? id : ki[0];
+}
+
+template <int NQ, int KM, int NBI>
+__global__ void __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2)))
+knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ scales,
+                   const float* __restrict__ xnorm, int nrows, int nblk,
+                   const float* __restrict__ qp, const float* __restrict__ qnorm, int nq, int dp,
+                   int nsplit, int64_t id_offset, int l2, float* __restrict__ cand_d,
+                   int64_t* __restrict__ cand_i, int ncand) {
+    // query in LDS, block b at b * kQB floats: the 16-B pad per block puts lane j's block
+    // (b = j + 16 bi) on 16-B bank slot j, so a ds_read_b128 lane group (16 distinct j) is
+    // conflict-free (unpadded, every block started on bank 0: 16-way conflicts)
+    constexpr int kQB = kBlk + 4;
+    constexpr int kQS = 16 * NBI * kQB;                // LDS floats per query (zero padded)
+    __shared__ __attribute__((aligned(16))) float sq[NQ * kQS];
+    __shared__ float fd[NQ][16][KM];
+    __shared__ int fi[NQ][16][KM];
+
+    const int split = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int j = lane & 15, g = lane >> 4;
+    const int64_t rowb = i8_row_bytes(nblk);
+    for (int i = tid; i < NQ * kQS; i += kWaves * 64) {
+        const int qi = i / kQS, r = i - qi * kQS, b = r / kQB, o = r - b * kQB, e = b * kBlk + o;
+        sq[i] = (qi < nq && o < kBlk && e < dp) ? qp[(int64_t)qi * dp + e] : 0.f;
+    }
+    float qn[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) qn[q] = (l2 && q < nq) ? qnorm[q] : 0.f;
+    __syncthreads();
+
+    float kd[KM];
+    int ki[KM];
+#pragma unroll
+    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+    const bool owner = j < NQ && j < nq;
+
+    const int ngroups = (nrows + kGroup - 1) / kGroup;
+    const int cnt = split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0;
+    // One 8-row group per wave step; two register sets, so the next group's loads are in flight
+    // while this one's products run (a single set left each wave idle for a whole HBM round trip
+    // per group: 4.7 TB/s with three waves per SIMD).
+    struct Grp {
+        uint4 cw[2][NBI][4];     // 2 rows x NBI blocks x 64 codes
+        float sc[2][NBI];
+        float xn[2];
+        int row[2];
+    };
+    auto load = [&](int li, Grp& G) __attribute__((always_inline)) {
+        const int m = split + li * nsplit;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            G.row[h] = m * kGroup + 4 * h + g;
+            const int rc = min(G.row[h], nrows - 1);
+#pragma unroll
+            for (int bi = 0; bi < NBI; ++bi) {
+                const int b = j + 16 * bi;
+                // chunk c of block b: slot 16 (4 bi + c) + j, so the 16 lanes of a row read 256
+                // contiguous bytes per load (slots of blocks >= nblk hold zeros)
+                const uint4* src = reinterpret_cast<const uint4*>(codes + (int64_t)rc * rowb) + 64 * bi + j;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) G.cw[h][bi][c] = src[16 * c];
+                G.sc[h][bi] = b < nblk ? scales[(int64_t)rc * nblk + b] : 0.f;
+            }
+            G.xn[h] = l2 ? xnorm[rc] : 0.f;
+        }
+    };
+    auto process = [&](Grp& G) __attribute__((always_inline)) {
+        float acc[2][NQ];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) acc[h][q] = 0.f;
+#pragma unroll
+        for (int bi = 0; bi < NBI; ++bi) {
+            const int b = j + 16 * bi;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                // chunk by chunk: the laundered offset keeps this chunk's query reads below the
+                // previous chunk's (pinned) accumulators, so at most one chunk's query values and
+                // converted codes are live (the compiler otherwise hoists every chunk's reads:
+                // 4 x NBI x 16 more registers)
+                int qoff = b * kQB + 16 * c;
+                asm volatile("" : "+v"(qoff));
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const float4* qv4 = reinterpret_cast<const float4*>(sq + q * kQS + qoff);
+                    const float4 qa = qv4[0], qb = qv4[1], qc = qv4[2], qd = qv4[3];
+                    const float qs[16] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w,
+                                          qc.x, qc.y, qc.z, qc.w, qd.x, qd.y, qd.z, qd.w};
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t wv[4] = {G.cw[h][bi][c].x, G.cw[h][bi][c].y, G.cw[h][bi][c].z,
+                                                G.cw[h][bi][c].w};
+                        float p0 = 0.f, p1 = 0.f;            // two 8-term chains per 16-element chunk
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) {
+                            p0 = fmaf(qs[t], (float)(signed char)(wv[t >> 2] >> (8 * (t & 3))), p0);
+                            p1 = fmaf(qs[8 + t], (float)(signed char)(wv[2 + (t >> 2)] >> (8 * (t & 3))), p1);
+                        }
+                        acc[h][q] = fmaf(G.sc[h][bi], p0 + p1, acc[h][q]);
+                    }
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[h][q]));
+            }
+        }
+        // keys; lane j (< NQ) of the row's group inserts query j's key (rows increase per lane)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float kv = INFINITY;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float dot = row16_sum(acc[h][q]);
+                float key = l2 ? fmaxf(fmaf(-2.f, dot, qn[q] + G.xn[h]), 0.f) : -dot;
+                kv = j == q ? key : kv;
+            }
+            kv = (owner && G.row[h] < nrows && kv < kd[KM - 1]) ? kv : INFINITY;
+            if (__any(kv != INFINITY)) insert_mono<KM>(kd, ki, kv, G.row[h]);
+        }
+    };
+    Grp A, B;
+    int li = wave;
+    if (li < cnt) load(li, A);
+    while (li < cnt) {
+        if (li + kWaves < cnt) load(li + kWaves, B);
+        process(A);
+        li += kWaves;
+        if (li >= cnt) break;
+        if (li + kWaves < cnt) load(li + kWaves, A);
+        process(B);
+        li += kWaves;
+    }
+
+    // fold the split's 16 lists of each query (4 waves x 4 row groups) into one list of KM
+    if (owner) {
+#pragma unroll
+        for (int p = 0; p < KM; ++p) {
+            fd[j][wave * 4 + g][p] = kd[p];
+            fi[j][wave * 4 + g][p] = ki[p];
+        }
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const int fq = lane >> 4, fl = lane & 15;              // query, list
+    if (fq >= NQ || fq >= nq) return;                    // (whole 16-lane groups leave together)
+    int pos = 0;
+    for (int p = 0; p < KM; ++p) {
+        float hk = pos < KM ? fd[fq][fl][pos] : INFINITY;
+        int hl = pos < KM ? fi[fq][fl][pos] : -1;
+        if (hl < 0) hk = INFINITY;
+        // min (key, label) over the group's 16 lanes; empty lists sort last
+        float bk = hk;
+        int bl = hl < 0 ? 0x7fffffff : hl;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            const float ok = __shfl_xor(bk, o, 16);
+            const int ol = __shfl_xor(bl, o, 16);
+            if (ok < bk || (ok == bk && ol < bl)) { bk = ok; bl = ol; }
+        }
+        const bool won = hk == bk && (hl < 0 ? 0x7fffffff : hl) == bl && bk != INFINITY;
+        if (won) ++pos;
+        if (fl == 0) {
+            const size_t o = (size_t)fq * ncand + (size_t)split * KM + p;
+            cand_d[o] = bk;
+            cand_i[o] = bk == INFINITY ? (int64_t)-1 : (int64_t)bl + id_offset;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* codes, float* scales,
+                          float* resid, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (nblk <= 0 || nblk > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(i8_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, xb, n, dp,
+                       nblk, codes, scales, resid);
+    return hipGetLastError();
+}
+
+hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
+    if (a.nblk <= 0 || a.nblk > 64 || a.nq < 1 || a.nsplit < 1) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);
+    const int nbi = (a.nblk + 15) / 16;
+#define IMGREC_I8(NQV, KMV, NBIV)                                                                 \
+    hipLaunchKernelGGL((knn_i8_scan_kernel<NQV, KMV, NBIV>), grid, block, 0, st, a.codes, a.scales, \
+                       a.xnorm, a.nrows, a.nblk, a.qp, a.qnorm, a.nq, a.dp, a.nsplit, a.id_offset,  \
+                       a.l2, a.cand_d, a.cand_i, a.ncand)
+#define IMGREC_I8_NBI(NQV, KMV)                                   \
+    do {                                                          \
+        switch (nbi) {                                            \
+            case 1: IMGREC_I8(NQV, KMV, 1); break;                \
+            case 2: IMGREC_I8(NQV, KMV, 2); break;                \
+            case 3: IMGREC_I8(NQV, KMV, 3); break;                \
+            default: IMGREC_I8(NQV, KMV, 4); break;               \
+        }                                                         \
+    } while (0)
+#define IMGREC_I8_KM(NQV)                                         \
+    do {                                                          \
+        if (a.km == 16) IMGREC_I8_NBI(NQV, 16);                   \
+        else if (a.km == 32) IMGREC_I8_NBI(NQV, 32);              \
+        else return hipErrorInvalidValue;                         \
+    } while (0)
+    if (a.nq == 1) IMGREC_I8_KM(1);
+    else if (a.nq == 2) IMGREC_I8_KM(2);
+    else if (a.nq <= 4) IMGREC_I8_KM(4);
+    else return hipErrorInvalidValue;
+#undef IMGREC_I8_KM
+#undef IMGREC_I8_NBI
+#undef IMGREC_I8
+    return hipGetLastError();
+}
+
+}  // namespace imgrec

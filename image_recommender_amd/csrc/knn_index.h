@@ -81,6 +81,10 @@ int split_kc(int k);
 float split_coef(int dp);
 float rerank_coef(int dp);
 float b16_acc_coef(int dpb);
+// int8 small-batch pass (knn_i8.hip): batches of at most kI8MaxQ queries, K' = kB16Cand
+constexpr int kI8MaxQ = 4;
+float i8_acc_coef(int nblk);
+Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus);
 constexpr int kB16Cand = 64;                   // K': candidates the bf16 pass hands to the rerank
 int b16_km(int k);
 
@@ -95,6 +99,11 @@ struct knn_index {
     uint32_t* xs = nullptr;  // cap x dp split-bf16 copy (built by the first split search)
     uint16_t* xh = nullptr;  // cap x dpb bf16 copy (b16_ok only)
     float* xr = nullptr;     // cap: |x - bf16(x)| per row (b16_ok only)
+    int8_t* x8 = nullptr;    // cap x nblk8*64 block-scaled int8 copy (built by the first i8 search)
+    float* x8s = nullptr;    // cap x nblk8 block scales
+    float* x8r = nullptr;    // cap: |x - s c| per row
+    float* x8r_max = nullptr; size_t x8r_max_cap = 0;   // device scalar, max of x8r
+    int nblk8 = 0;           // 64-element blocks per row (d <= 4096)
     float* xn_max = nullptr; // device scalar, max |x|^2 (refreshed when rows change)
     float* xr_max = nullptr; // device scalar, max |x - bf16(x)|
     int dpb = 0;             // bf16 row stride (elements)
@@ -164,6 +173,7 @@ int fence_end(knn_index* ix, hipStream_t st);
 int reserve_rows(knn_index* ix, int64_t need, hipStream_t st);
 int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st);
 int ensure_split(knn_index* ix, hipStream_t st);
+int ensure_i8(knn_index* ix, hipStream_t st);
 int create_single(int d, int metric, int device, knn_index** out);
 void free_single(knn_index* ix);
 // knn_search.cpp
@@ -172,6 +182,7 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
 int read_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int64_t* first_fail,
                       float* ratio);
 bool use_b16(const knn_index* ix, int64_t nq, int k);
+bool use_i8(const knn_index* ix, int64_t nq, int k);
 // knn_largek.hip
 int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                   hipStream_t st);

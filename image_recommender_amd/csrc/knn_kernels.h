@@ -11,6 +11,7 @@ namespace imgrec {
 constexpr int kModeF32 = 0;     // exact fp32 rows, v_mfma_f32_32x32x2_f32
 constexpr int kModeSplit = 1;   // split-bf16 rows (hi, lo), three bf16 MFMAs per product
 constexpr int kModeBF16 = 2;    // bf16 rows, one bf16 MFMA per product (candidate pass)
+constexpr int kModeI8 = 3;      // block-scaled int8 rows, fp32 VALU dot (small-batch candidate pass)
 
 // Arguments of one fused distance + top-k launch.
 struct TileArgs {
@@ -35,7 +36,7 @@ struct TileArgs {
 
 // One rerank + certificate launch over merged candidate-pass candidates (knn_refine.hip).
 struct RerankArgs {
-    int mode;                   // kModeSplit or kModeBF16: which error bound certifies
+    int mode;                   // kModeSplit, kModeBF16 or kModeI8: which error bound certifies
     const float* qp;            // fp32 padded queries, nq x dp
     const float* qnorm;
     int dp;
@@ -52,8 +53,9 @@ struct RerankArgs {
                                 // (the packed-list candidate kernel); 0 = exact approximate keys
     float c_split, c_fp;        // relative error-bound coefficients (see knn_capi.cpp); for
                                 // kModeBF16 c_split is the MFMA accumulation coefficient
-    const float* q_resid;       // kModeBF16: |q - bf16(q)| per query
-    const float* xr_max;        // kModeBF16: device scalar, max over rows of |x - bf16(x)|
+    const float* q_resid;       // kModeBF16: |q - bf16(q)| per query (kModeI8: NULL, fp32 query)
+    const float* xr_max;        // kModeBF16: device scalar, max over rows of |x - bf16(x)|;
+                                // kModeI8: max over rows of |x - s c| (the int8 copy's residual)
     const float* floor;         // per query: smallest key any row outside the candidates can
                                 // have besides the K'-th candidate's (merge "floor"), or NULL
     float* D;
@@ -147,6 +149,28 @@ constexpr int kB16NS = IMGREC_B16_NS, kB16WGPCU = IMGREC_B16_WGPCU, kB16Pad = 64
 #endif
 constexpr int kB16PackMaxIB = IMGREC_B16_PACK_MAXIB;
 constexpr int kB16BigRows = 256, kB16BigQueries = 256, kB16BigMinQ = IMGREC_B16_BIG_MINQ;
+
+// Small-batch candidate pass on the block-scaled int8 copy (knn_i8.hip): per (query, row split)
+// the km best approximate keys, nq <= 4 queries in one launch, nsplit workgroups.
+struct I8Args {
+    const int8_t* codes;        // cap x nblk*64 codes
+    const float* scales;        // cap x nblk block scales
+    const float* xnorm;         // |x|^2 per stored row (exact)
+    int nrows, nblk;
+    const float* qp;            // fp32 queries, nq x dp
+    const float* qnorm;
+    int nq, dp, km, nsplit, l2;
+    int64_t id_offset;
+    float* cand_d;              // nq x ncand keys, one sorted list of km per split
+    int64_t* cand_i;
+    int ncand;
+};
+// bytes per row of the int8 copy: 16-block groups of 1 KiB, block b's 4 chunks at 16-B slots
+// 16 (4 (b / 16) + c) + b % 16 (one contiguous 256-B load per 16-lane row group in the scan)
+__host__ __device__ inline int64_t i8_row_bytes(int nblk) { return (int64_t)1024 * ((nblk + 15) / 16); }
+hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* codes, float* scales,
+                          float* resid, hipStream_t st);
+hipError_t launch_i8_scan(const I8Args& a, hipStream_t st);
 
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);

@@ -2,6 +2,7 @@
 // error-bound coefficients of the candidate paths' certificate (DESIGN.md "Launch plan",
 // "bf16 path", "Split path").
 #include <cmath>
+#include <cstdlib>
 
 #include "knn_index.h"
 
@@ -78,6 +79,46 @@ float rerank_coef(int dp) {
 float b16_acc_coef(int dpb) {
     return (float)(1.02 * (5.0 * (dpb / 16) + 16.0) * std::ldexp(1.0, -23));
 }
+// int8 small-batch pass (knn_i8.hip): per lane, two 8-term fp32 FMA chains per 16-element chunk
+// and their sum, the block scale folded into the lane's accumulator by one FMA per chunk (4 chunks
+// x ceil(nblk/16) blocks), then the 16-lane DPP sum: 1.02 * gamma_n with
+// n = 8 + 1 + 4 ceil(nblk/16) + 4 (+ 3 slack), relative to |q| |x~| (the codes and scales are
+// exact in fp32; the query is not rounded).  Unit roundoff 2^-23 as above.
+float i8_acc_coef(int nblk) {
+    return (float)(1.02 * (16.0 + 4.0 * ((nblk + 15) / 16)) * std::ldexp(1.0, -23));
+}
+
+// int8-path geometry: one workgroup per row split, kI8WGPCU per CU, all of the batch's queries
+// in each; one folded list of km per (query, split)
+// (two 4-wave workgroups per CU are resident at the kernel's 222 VGPRs; three per CU, i.e. a
+// second partial round, measured faster at nq = 1 / 2: 0.366 / 0.375 vs 0.386 / 0.399 ms kernel,
+// profiles/r03/i8_small_batch/sweep.jsonl; IMGREC_I8_WGPCU overrides for measurements)
+static int i8_wgpcu() {
+    static const int v = [] {
+        const char* e = std::getenv("IMGREC_I8_WGPCU");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 && x <= 16 ? x : 3;
+    }();
+    return v;
+}
+Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus) {
+    const int kI8WGPCU = i8_wgpcu();
+    Plan p{};
+    p.km = b16_km(k);
+    p.wr = 1;
+    p.wq = 1;
+    p.bm = 8;
+    p.bq = (int)nq;
+    p.nqb = 1;
+    p.nq_pad = (int)nq;
+    const int64_t groups = (ntotal + 7) / 8;
+    p.ntiles = (int)groups;
+    p.nsplit = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)cus * kI8WGPCU, groups));
+    p.ncand = p.nsplit * p.km;
+    p.wgs = p.nsplit;
+    return p;
+}
+
 // per-lane list length of the generic bf16 tile (the merge floor covers what a lane list drops)
 int b16_km(int k) { return k <= 16 ? 16 : 32; }
 

@@ -70,6 +70,10 @@ int refresh_maxima(knn_index* ix, hipStream_t st) {
         if ((rc = grow(&ix->xr_max, &ix->xr_max_cap, 1)) != KNN_OK) return rc;
         KNN_HIP(launch_max_norm(ix->xr, ix->ntotal, ix->xr_max, st));
     }
+    if (ix->x8) {
+        if ((rc = grow(&ix->x8r_max, &ix->x8r_max_cap, 1)) != KNN_OK) return rc;
+        KNN_HIP(launch_max_norm(ix->x8r, ix->ntotal, ix->x8r_max, st));
+    }
     ix->xn_max_stale = false;
     return KNN_OK;
 }
@@ -197,6 +201,53 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
 }
 
+// Block-scaled int8 candidates (fp32 VALU dot, batches of <= kI8MaxQ queries) + exact fp32
+// rerank of K' = 64 + certificate: the bf16 path's chain with the int8 copy's bound.
+int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
+             int64_t* I, hipStream_t st, bool timed, bool first) {
+    const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
+    const int kc = kB16Cand;
+    const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus);
+    int rc;
+    if ((rc = ensure_i8(ix, st)) != KNN_OK) return rc;
+    if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
+    if ((rc = grow_stats(ix, nq, st)) != KNN_OK) return rc;
+    I8Args a{};
+    a.codes = ix->x8; a.scales = ix->x8s; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
+    a.nblk = ix->nblk8; a.qp = qpad; a.qnorm = qnorm; a.nq = (int)nq; a.dp = ix->dp; a.km = p.km;
+    a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
+    a.cand_i = ix->cand_i; a.ncand = p.ncand;
+    hipEvent_t e1 = nullptr;
+    if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+    KNN_HIP(launch_i8_scan(a, st));
+    if (e1) KNN_HIP(hipEventRecord(e1, st));
+    const int nlists = p.nsplit, ngrp = (nlists + 63) / 64;
+    if (ngrp > 1) {
+        if ((rc = grow(&ix->mws_d, &ix->mws_d_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
+    }
+    KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, p.km, p.ncand, p.km, kc,
+                                    ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
+                                    ix->mws_d, ix->mws_i, ix->mws_f, st));
+    RerankArgs r{};
+    r.mode = kModeI8;
+    r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
+    r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
+    r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = i8_acc_coef(ix->nblk8);
+    r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+    r.c_trunc = 0.f;
+    r.q_resid = nullptr; r.xr_max = ix->x8r_max; r.floor = ix->floor;
+    r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = p.km;
+    r.raw_stride_q = p.ncand;
+    return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
+}
+
 // Split-bf16 candidates + exact rerank + certificate.
 int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
                 int64_t* I, hipStream_t st, bool timed, bool first) {
@@ -248,8 +299,19 @@ constexpr int64_t kB16MinRowsLarge = 16384, kB16MinRowsSmall = 131072;
 bool use_b16(const knn_index* ix, int64_t nq, int k) {
     if (!ix->b16_ok || k > KNN_MAX_K) return false;
     if (ix->mode == KNN_SEARCH_BF16) return true;
-    if (ix->mode != KNN_SEARCH_AUTO) return false;
+    // (I8 mode: batches the int8 path does not take are served as AUTO serves them)
+    if (ix->mode != KNN_SEARCH_AUTO && ix->mode != KNN_SEARCH_I8) return false;
     return ix->ntotal >= (nq > 128 ? kB16MinRowsLarge : kB16MinRowsSmall);
+}
+
+// AUTO: batches of <= kI8AutoQ queries on an index the bf16 path would serve as small (the int8
+// copy streams about half of the bf16 copy's bytes; its VALU dot costs grow with the batch)
+constexpr int kI8AutoQ = 2;
+bool use_i8(const knn_index* ix, int64_t nq, int k) {
+    if (ix->nblk8 <= 0 || k > KNN_MAX_K || nq > kI8MaxQ) return false;
+    if (ix->mode == KNN_SEARCH_I8) return true;
+    if (ix->mode != KNN_SEARCH_AUTO) return false;
+    return nq <= kI8AutoQ && ix->ntotal >= kB16MinRowsSmall;
 }
 
 bool use_split(const knn_index* ix, int64_t nq, int k) {
@@ -257,7 +319,7 @@ bool use_split(const knn_index* ix, int64_t nq, int k) {
     if (ix->mode == KNN_SEARCH_SPLIT) return true;
     // auto (when the bf16 path is unavailable): batches the (1,4) plan covers, corpora with
     // enough rows to amortise the rerank
-    return ix->mode == KNN_SEARCH_AUTO && nq > 128 && ix->ntotal >= 16384;
+    return (ix->mode == KNN_SEARCH_AUTO || ix->mode == KNN_SEARCH_I8) && nq > 128 && ix->ntotal >= 16384;
 }
 
 int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
@@ -277,19 +339,23 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     bool first_cand = true;
     for (int64_t c0 = 0; c0 < nq; c0 += kQueryChunk) {
         const int64_t cn = std::min(kQueryChunk, nq - c0);
-        const bool b16 = use_b16(ix, cn, k);
-        const bool split = !b16 && use_split(ix, cn, k);
+        const bool i8 = use_i8(ix, cn, k);
+        const bool b16 = !i8 && use_b16(ix, cn, k);
+        const bool split = !i8 && !b16 && use_split(ix, cn, k);
         // padding: the query tile of the plan this chunk will run (and the exact re-run's 32)
-        const Plan p = b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
+        const Plan p = i8 ? make_i8_plan(ix->ntotal, cn, k, ix->cus)
+                     : b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                      : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                              : make_plan(ix->ntotal, cn, k, ix->cus);
         const int64_t nq_pad = p.nq_pad;
         int rc;
-        if (c0 == 0) ix->last_path = b16 ? 2 : (split ? 1 : 0);
+        if (c0 == 0) ix->last_path = i8 ? 3 : (b16 ? 2 : (split ? 1 : 0));
         if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;
         bool q_ready = false;
-        if (b16 && ix->dpb <= 4096) {   // fused query prep: fp32 padded rows + norms + bf16 + residuals
+        // fused query prep: fp32 padded rows + norms + bf16 + residuals (the int8 path uses its
+        // fp32 rows and norms: one short pass instead of rows_ingest's latency-bound row loop)
+        if ((b16 || i8) && ix->dpb <= 4096) {
             if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)nq_pad * ix->dpb)) != KNN_OK) return rc;
             if ((rc = grow(&ix->q_resid, &ix->q_resid_cap, (size_t)nq_pad)) != KNN_OK) return rc;
             KNN_HIP(launch_query_prep_b16(q + c0 * ix->d, cn, ix->d, ix->dp, ix->dpb, nq_pad,
@@ -301,8 +367,9 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         }
         float* Dc = D + c0 * k;
         int64_t* Ic = I + c0 * k;
-        if (b16 || split) {
-            rc = b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, q_ready, first_cand)
+        if (i8 || b16 || split) {
+            rc = i8 ? i8_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, first_cand)
+               : b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, q_ready, first_cand)
                      : split_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, first_cand);
             first_cand = false;
         } else {

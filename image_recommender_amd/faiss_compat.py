@@ -202,7 +202,8 @@ class Index:
 
     # -- search arithmetic (extension; include/imgrec_knn.h knn_search_mode) -------------------
     SEARCH_MODES = {"auto": _lib.KNN_SEARCH_AUTO, "exact": _lib.KNN_SEARCH_EXACT,
-                    "split": _lib.KNN_SEARCH_SPLIT, "bf16": _lib.KNN_SEARCH_BF16}
+                    "split": _lib.KNN_SEARCH_SPLIT, "bf16": _lib.KNN_SEARCH_BF16,
+                    "i8": _lib.KNN_SEARCH_I8}
 
     @property
     def search_mode(self) -> str:

@@ -1,0 +1,183 @@
+"""Parity tests of the int8 small-batch candidate path (include/imgrec_knn.h KNN_SEARCH_I8, the AUTO
+default for batches of <= 2 queries on an index of >= 131072 rows; csrc/knn_i8.hip).
+
+The int8 path scores rows on a block-scaled int8 copy (one fp32 scale per 64 elements) with an
+fp32 query, reranks K' = 64 candidates in exact fp32 and certifies per query, from the stored
+residual norms |x - s c|, that no row outside the candidates can rank before a returned one;
+uncertified queries get the second chance over the per-split lists, then the exact re-run.  The
+results must satisfy the SAME contract as the exact path (tests/knn_check.py against the float64
+oracle): this is the arithmetic behind the reference CLI's one-query index.search
+(main/search_from_image.py:247).
+"""
+import numpy as np
+import pytest
+
+from tests.datagen import concat_rows, mixture
+from tests.knn_check import check_knn
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def faiss(gpu):
+    from image_recommender_amd import faiss_compat
+    return faiss_compat
+
+
+def _lib():
+    from image_recommender_amd import _lib
+    return _lib.load()
+
+
+def _index(faiss, d, metric):
+    if metric == "l2":
+        return faiss.IndexFlatL2(d)
+    if metric == "ip":
+        return faiss.IndexFlatIP(d)
+    return faiss.IndexFlat(d, faiss.METRIC_COSINE)
+
+
+def _stats(idx, nq):
+    ncand, reruns, ratio = idx.search_stats(with_error=True)
+    assert ncand == nq
+    assert 0.0 <= ratio < 1.0, ratio
+    return reruns
+
+
+@pytest.mark.parametrize("d", [64, 100, 300, 768, 1024, 1968])
+@pytest.mark.parametrize("nq", [1, 2, 3, 4])
+def test_i8_l2_shapes(faiss, d, nq):
+    xb = mixture(6001, d, centres=50, seed=d)                 # not a multiple of the 8-row group
+    xq = mixture(nq, d, centres=50, seed=d + 1)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, 10)
+    assert _lib().knn_last_path(idx.handle) == 3
+    _stats(idx, nq)
+    # (at d >= 1024 the mixture's neighbours crowd inside the fp32 tie window: fewer ranks are
+    # tie-free, every label is still checked against its exact distance)
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5 if d < 1024 else 0.25)
+
+
+@pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 32])
+def test_i8_k_values(faiss, k):
+    xb = mixture(9000, 512, centres=80, seed=k)
+    xq = mixture(2, 512, centres=80, seed=k + 100)
+    idx = faiss.IndexFlatL2(512)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, k)
+    _stats(idx, 2)
+    check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("metric", ["ip", "cosine"])
+def test_i8_ip_and_cosine(faiss, metric):
+    xb = mixture(7000, 384, centres=40, seed=5)
+    xq = mixture(2, 384, centres=40, seed=6)
+    idx = _index(faiss, 384, metric)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, 10)
+    _stats(idx, 2)
+    check_knn(D, I, xb, xq, 10, metric, min_exact_frac=0.5)
+    assert np.all(np.diff(D, axis=1) <= 0)
+
+
+def test_i8_concat_layout_self_query(faiss):
+    """The reference's stored layout (colour 48 | SIFT 128 | DreamSim 1792, unit-norm parts), a
+    stored row as the query: the row itself first at distance ~0."""
+    xb = concat_rows(20000, seed=11)
+    idx = faiss.IndexFlatL2(xb.shape[1])
+    idx.add(xb)
+    idx.search_mode = "i8"
+    for qi in (0, 12345):
+        D, I = idx.search(xb[qi:qi + 1], 10)
+        assert I[0, 0] == qi and D[0, 0] < 1e-4
+        check_knn(D, I, xb, xb[qi:qi + 1], 10, "l2", min_exact_frac=0.5)
+
+
+def test_i8_auto_picks_int8_for_single_queries(faiss):
+    """AUTO: one or two queries on >= 131072 rows take the int8 path, three take the bf16 path."""
+    d = 256
+    xb = mixture(140000, d, centres=200, seed=3)
+    xq = mixture(3, d, centres=200, seed=4)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    from oracle.flat_knn import search_exact
+    orc = search_exact(xb, xq, 11, "l2")
+    for nq, path in ((1, 3), (2, 3), (3, 2)):
+        D, I = idx.search(xq[:nq], 10)
+        assert _lib().knn_last_path(idx.handle) == path
+        check_knn(D, I, xb, xq[:nq], 10, "l2", min_exact_frac=0.5,
+                  oracle=(orc[0][:nq], orc[1][:nq]))
+
+
+def test_i8_rows_added_after_the_copy_exists(faiss):
+    """Adds after the first int8 search (copy built) extend it, across a capacity regrowth."""
+    d = 192
+    xb = mixture(30000, d, centres=60, seed=8)
+    xq = mixture(2, d, centres=60, seed=9)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb[:5000])
+    idx.search_mode = "i8"
+    idx.search(xq, 10)                                        # builds the int8 copy of 5000 rows
+    idx.add(xb[5000:12000])
+    idx.add(xb[12000:])                                       # regrowth
+    D, I = idx.search(xq, 10)
+    _stats(idx, 2)
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+    idx.reset()
+    idx.add(xb[:3000])
+    D, I = idx.search(xq, 10)
+    check_knn(D, I, xb[:3000], xq, 10, "l2", min_exact_frac=0.5)
+
+
+def test_i8_many_near_ties_fall_back_exactly(faiss):
+    """200 copies of one row plus tiny perturbations around the query: far more rows inside the
+    certificate's band than K' = 64, so the first certificate fails; the second chance / exact
+    re-run must still return the exact answer."""
+    d = 128
+    rng = np.random.default_rng(5)
+    base = mixture(20000, d, centres=30, seed=10)
+    q = base[7].copy()
+    near = q[None, :] + rng.normal(0, 1e-4, size=(200, d)).astype(np.float32)
+    xb = np.concatenate([base, near]).astype(np.float32)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(q[None, :], 10)
+    # every rank sits in a tie window by construction: positions and exact distances are checked
+    check_knn(D, I, xb, q[None, :], 10, "l2", min_exact_frac=0.0)
+    assert set(I[0].tolist()) <= set(range(20000, 20200)) | {7}
+
+
+def test_i8_clustered_storage(faiss):
+    """Rows stored cluster by cluster (similar images on adjacent rows, as a folder-ordered
+    database numbers them): the 8-row groups interleaved over the splits keep every split's list
+    from filling with one cluster."""
+    d = 256
+    xb = mixture(60000, d, centres=30, seed=21)
+    rng = np.random.default_rng(0)
+    lab = np.argsort(((xb @ rng.normal(size=(d, 30))).argmax(1)), kind="stable")
+    xb = np.ascontiguousarray(xb[lab])
+    xq = xb[[5, 40000]] + 0.01
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, 10)
+    reruns = _stats(idx, 2)
+    assert reruns == 0
+    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+
+
+def test_i8_mode_batch_above_four_served_as_auto(faiss):
+    xb = mixture(5000, 128, centres=20, seed=1)
+    xq = mixture(40, 128, centres=20, seed=2)
+    idx = faiss.IndexFlatL2(128)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, 5)
+    assert _lib().knn_last_path(idx.handle) != 3
+    check_knn(D, I, xb, xq, 5, "l2", min_exact_frac=0.5)
