@@ -100,6 +100,30 @@ def test_cfg3_full_size_auto_bf16(faiss, cfg3):
     np.testing.assert_array_equal(D2, Dh)
 
 
+def test_cfg3_full_size_single_queries_int8(faiss, cfg3):
+    """The reference CLI's regime at full size: one query, and two, per search through AUTO on the
+    1M x 1968 corpus take the int8 small-batch path (knn_i8.hip); 16 sampled queries searched one
+    at a time and 8 pairs, against the float64 oracle, every query certified on the first pass."""
+    from image_recommender_amd import _lib
+    idx, xq = cfg3["idx"], cfg3["xq"]
+    Dg, Ig = cfg3["oracle"]
+    for r in range(0, len(cfg3["sel"]), 2):
+        s = cfg3["sel"][r]
+        D, I = idx.search(xq[s:s + 1], K)
+        assert _lib.load().knn_last_path(idx.handle) == 3
+        st = idx.certificate_stats()
+        assert st["candidate_queries"] == 1 and st["exact_reruns"] == 0
+        assert 0.0 <= st["max_err_over_bound"] < 1.0
+        check_knn(D, I, cfg3["xb"], xq[s:s + 1], K, "l2", min_exact_frac=0.5,
+                  oracle=(Dg[r:r + 1], Ig[r:r + 1]))
+    for r in range(0, len(cfg3["sel"]) - 1, 4):
+        pair = cfg3["sel"][[r, r + 1]]
+        D, I = idx.search(xq[pair], K)
+        assert _lib.load().knn_last_path(idx.handle) == 3
+        check_knn(D, I, cfg3["xb"], xq[pair], K, "l2", min_exact_frac=0.5,
+                  oracle=(Dg[r:r + 2], Ig[r:r + 2]))
+
+
 def test_cfg3_full_size_exact_kernel(faiss, cfg3):
     """The fp32 exact kernel on the same corpus (128 queries: the (1,4) tile), sampled queries."""
     idx, xq = cfg3["idx"], cfg3["xq"]
