@@ -146,7 +146,10 @@ struct knn_index {
     float* fb_cd = nullptr; size_t fb_cd_cap = 0;
     int64_t* fb_ci = nullptr; size_t fb_ci_cap = 0;
     int* tail_ctl = nullptr; size_t tail_ctl_cap = 0;   // tail claim counters + block tickets
-    // host-path staging
+    // host-path staging (device side), and page-locked host buffers for small searches
+    float* pq = nullptr; size_t pq_cap = 0;        // hipHostMalloc'ed (caps in bytes)
+    float* pd = nullptr; size_t pd_cap = 0;
+    int64_t* pi = nullptr; size_t pi_cap = 0;
     float* hq = nullptr; size_t hq_cap = 0;
     float* hd = nullptr; size_t hd_cap = 0;
     int64_t* hi = nullptr; size_t hi_cap = 0;

@@ -26,7 +26,7 @@ torch.cuda.synchronize()
 qd = bench.gen_queries(torch, cfg, cent, 1024, dev, 3)
 qh = qd.cpu().numpy()
 idx = shard.index
-for nq in (1, 1024):
+for nq in (1, 2, 1024):
     x = np.ascontiguousarray(qh[:nq])
     for _ in range(3):
         idx.search(x, 10)
