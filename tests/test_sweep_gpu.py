@@ -68,6 +68,47 @@ def test_random_case_matches_oracle(faiss, n, d, nq, k, metric, mode, adds, seed
     check_knn(D, I, xb, xq, k, metric, min_exact_frac=0.0)
 
 
+def _i8_cases(n_cases=24, seed=2027):
+    """The int8 small-batch path (search_mode "i8", knn_i8.hip): batches of 1-4 queries (and 5, 40:
+    served as AUTO), tiny and ragged corpora, d below the path's 64 (refused at the setter), k past
+    the fused lists (the large-k path takes it)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n_cases):
+        n = int(rng.choice([1, 5, 8, 9, 255, 1000, 4099, 20000, 70000]))
+        d = int(rng.choice([16, 64, 65, 130, 256, 300, 512, 1024, 1968, 2500]))
+        nq = int(rng.choice([1, 1, 2, 2, 3, 4, 5, 40]))
+        k = int(rng.choice([1, 3, 10, 16, 17, 32, 40]))
+        metric = _METRICS[int(rng.integers(0, 3))]
+        adds = int(rng.choice([1, 1, 3]))
+        if n * d > 40_000_000:
+            n = 40_000_000 // d
+        out.append(pytest.param(n, d, nq, k, metric, adds, 3000 + i, id=f"i{i}"))
+    return out
+
+
+@pytest.mark.parametrize("n,d,nq,k,metric,adds,seed", _i8_cases())
+def test_random_i8_case_matches_oracle(faiss, n, d, nq, k, metric, adds, seed):
+    from image_recommender_amd import _lib
+    from image_recommender_amd._lib import KnnError
+    xb = mixture(n, d, centres=max(2, min(60, n // 4)), seed=seed)
+    xq = mixture(nq, d, centres=max(2, min(60, n // 4)), seed=seed + 1)
+    idx = (faiss.IndexFlatL2(d) if metric == "l2" else faiss.IndexFlatIP(d) if metric == "ip"
+           else faiss.IndexFlat(d, faiss.METRIC_COSINE))
+    if d < 64:
+        with pytest.raises(KnnError):
+            idx.search_mode = "i8"
+    else:
+        idx.search_mode = "i8"
+    for part in np.array_split(xb, adds):
+        if len(part):
+            idx.add(np.ascontiguousarray(part))
+    D, I = idx.search(xq, k)
+    if d >= 64 and nq <= 4 and k <= 32:
+        assert _lib.load().knn_last_path(idx.handle) == 3
+    check_knn(D, I, xb, xq, k, metric, min_exact_frac=0.0)
+
+
 def test_k_above_limit_raises(faiss):
     """k > KNN_MAX_K_LARGE is refused loudly."""
     from image_recommender_amd._lib import KNN_MAX_K_LARGE
