@@ -227,7 +227,8 @@ __global__ void __launch_bounds__(512, 2)
 knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ xnorm, int nrows,
                      int dw, const uint32_t* __restrict__ qh, const float* __restrict__ qnorm, int nq,
                      int nsplit, int nqb, int64_t id_offset, float* __restrict__ cand_d,
-                     int64_t* __restrict__ cand_i, int ncand, int ib) {
+                     int64_t* __restrict__ cand_i, int ncand, int ib, uint32_t* __restrict__ sync,
+                     uint32_t epoch, int lag) {
     __shared__ __attribute__((aligned(16))) char smem[kLDS];
 
     // XCD-aware bijective block -> (query block, row split) map, as knn_b16_tile_kernel
@@ -239,6 +240,9 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
     const int qbg = wgid / (nsplit * G), rem = wgid - qbg * (nsplit * G);
     const int split = rem / G;
     const int qb = qbg * G + rem % G;
+    // the G query-block workgroups of this row split: wgids sib0 .. sib0 + G - 1
+    const int sib0 = wgid - rem % G;
+    bool sync_on = sync != nullptr && G == kG;
     const int ngroups = (nrows + kRPP - 1) / kRPP;
     const int cnt = split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0;
     const int t0 = 0, t1 = (cnt + kGPT - 1) / kGPT;
@@ -538,6 +542,29 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
             }
         }
         B16W_STAMP(2 * (t - t0) + 1);
+        // sibling lockstep (TileArgs::sync): publish this tile, wait (bounded) until the G
+        // workgroups of this row split have all finished it (minus the lag), so they enter the
+        // next tile together and its corpus stages are fetched from HBM once, then served from
+        // L2 to the other three.  Only lane 0 of wave 0 waits; the other waves run on into the
+        // next tile and stop at its first stage barrier.  A sibling that never shows up (not
+        // resident) turns the wait off for the rest of the launch.
+        if (sync_on && wave == 0 && t + 1 < t1) {
+            if (lane == 0) {
+                const uint32_t mine = (epoch << 16) + (uint32_t)(t - t0) + 1u;
+                __hip_atomic_store(sync + wgid, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t want = mine - (uint32_t)lag;
+                for (int spin = 0;; ++spin) {
+                    bool ok = true;
+#pragma unroll
+                    for (int s2 = 0; s2 < kG; ++s2)
+                        ok = ok && (int)(__hip_atomic_load(sync + sib0 + s2, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) - want) >= 0;
+                    if (ok) break;
+                    if (spin >= 4096) { sync_on = false; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        }
 #ifdef IMGREC_B16_STAMPS
         if (stamp_on && lane == 0) g_b16w_stamps[wave * 256 + 128 + (t - t0)] = (unsigned long long)nit;
 #endif
@@ -608,7 +635,7 @@ hipError_t launch_b16_wide(const TileArgs& a, hipStream_t st) {
 #define IMGREC_LAUNCH_B16W(KMV, L2V, PK)                                                             \
     hipLaunchKernelGGL((knn_b16w_tile_kernel<KMV, L2V, PK>), grid, block, 0, st, xh, a.xnorm,      \
                        a.nrows, a.dp, qh, a.qnorm, a.nq, a.nsplit, a.nqb, a.id_offset, a.cand_d,   \
-                       a.cand_i, a.ncand, a.ib)
+                       a.cand_i, a.ncand, a.ib, a.sync, a.epoch, a.sync_lag)
 #define IMGREC_LAUNCH_B16W_K(KMV, PK)                                                               \
     do { if (a.metric == 1) IMGREC_LAUNCH_B16W(KMV, 1, PK); else IMGREC_LAUNCH_B16W(KMV, 0, PK); } while (0)
     if (a.km == 8) {

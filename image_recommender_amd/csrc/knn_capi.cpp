@@ -239,6 +239,7 @@ void free_single(knn_index* ix) {
     for (void* p : {(void*)ix->xh, (void*)ix->xr, (void*)ix->xr_max, (void*)ix->qb16,
                     (void*)ix->q_resid, (void*)ix->floor, (void*)ix->mws_d, (void*)ix->mws_i,
                     (void*)ix->mws_f, (void*)ix->stat, (void*)ix->fb_cd, (void*)ix->fb_ci,
+                    (void*)ix->b16_sync,
                     (void*)ix->tail_ctl, (void*)ix->chance})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,

@@ -139,6 +139,8 @@ struct knn_index {
     float* mws_d = nullptr; size_t mws_d_cap = 0;          // two-level candidate merge workspace
     int64_t* mws_i = nullptr; size_t mws_i_cap = 0;
     float* mws_f = nullptr; size_t mws_f_cap = 0;
+    uint32_t* b16_sync = nullptr; size_t b16_sync_cap = 0;   // 256 x 256 kernel sibling progress
+    uint32_t b16_epoch = 0;
     size_t xr_max_cap = 0;
     // exact re-run workspace (device-planned: queries, candidate lists, plan)
     float* fb_q = nullptr; size_t fb_q_cap = 0;

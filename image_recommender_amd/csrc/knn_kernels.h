@@ -32,6 +32,12 @@ struct TileArgs {
     int64_t* cand_i;            // nq x ncand labels
     int ncand;
     int ib = 0;                 // 256 x 256 bf16 kernel: > 0 = packed lists with ib index bits
+    // 256 x 256 bf16 kernel, optional: per-workgroup tile progress (one uint32 per workgroup,
+    // values (epoch << 16) + tiles done), so the query-block workgroups that share a row split
+    // start every tile together and read its corpus stages from L2 once (NULL = off)
+    uint32_t* sync = nullptr;
+    uint32_t epoch = 0;
+    int sync_lag = 0;           // tiles a workgroup may run ahead of its slowest sibling
 };
 
 // One rerank + certificate launch over merged candidate-pass candidates (knn_refine.hip).

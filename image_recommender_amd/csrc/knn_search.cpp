@@ -12,6 +12,7 @@
 // the device: the count never travels to the host, so knn_search_device enqueues a whole search
 // without waiting for the GPU.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "knn_index.h"
@@ -149,6 +150,17 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     return KNN_OK;
 }
 
+// Sibling lockstep of the 256 x 256 bf16 kernel (TileArgs::sync): IMGREC_B16W_SYNC_LAG = the
+// tiles a workgroup may run ahead of the slowest workgroup of its row split; unset or negative =
+// off.
+int b16_sync_lag() {
+    static const int v = [] {
+        const char* e = std::getenv("IMGREC_B16W_SYNC_LAG");
+        return e && *e ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
 // bf16 candidates (one bf16 MFMA per product) + exact fp32 rerank of K' = 64 + certificate.
 int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
               int64_t* I, hipStream_t st, bool timed, bool q_ready, bool first) {
@@ -175,6 +187,18 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     a.nq = (int)nq; a.metric = kmetric; a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb;
     a.id_offset = ix->id_offset; a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand;
     a.ib = p.big ? p.ib : 0;
+    if (p.big && b16_sync_lag() >= 0) {
+        // sibling lockstep of the 256 x 256 kernel: progress slots zeroed once, a new epoch per
+        // launch (values of earlier launches compare as "not yet")
+        const size_t cap0 = ix->b16_sync_cap;
+        if ((rc = grow(&ix->b16_sync, &ix->b16_sync_cap, (size_t)p.wgs)) != KNN_OK) return rc;
+        if (ix->b16_sync_cap != cap0)
+            KNN_HIP(hipMemsetAsync(ix->b16_sync, 0, ix->b16_sync_cap * sizeof(uint32_t), st));
+        ix->b16_epoch = (ix->b16_epoch + 1) & 0xffffu;
+        a.sync = ix->b16_sync;
+        a.epoch = ix->b16_epoch;
+        a.sync_lag = b16_sync_lag();
+    }
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
     KNN_HIP(p.big ? launch_b16_big(a, st) : launch_tile_topk(a, st));
