@@ -240,7 +240,8 @@ void free_single(knn_index* ix) {
                     (void*)ix->q_resid, (void*)ix->floor, (void*)ix->mws_d, (void*)ix->mws_i,
                     (void*)ix->mws_f, (void*)ix->stat, (void*)ix->fb_cd, (void*)ix->fb_ci,
                     (void*)ix->b16_sync,
-                    (void*)ix->tail_ctl, (void*)ix->chance})
+                    (void*)ix->tail_ctl, (void*)ix->chance, (void*)ix->sc_key, (void*)ix->sc_lab,
+                    (void*)ix->sc_meta, (void*)ix->sc_done})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
                     (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,

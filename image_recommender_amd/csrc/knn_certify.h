@@ -123,117 +123,6 @@ __device__ __forceinline__ float rerank_key(float ip, float qn, float xnr, int m
 
 
 // ---------------------------------------------------------------------------------------------
-// Second chance for one query the rerank could not certify (item `item` of chance_list): every
-// entry of the candidate pass's per-split lists with approximate key <= the prefix limit (those
-// above it cannot reach the top k) is reranked, and the certificate is re-run against the list
-// floor alone — the smallest last key of a full list, below which no row outside all lists can
-// be.  NW waves per workgroup.  A query it cannot settle goes to the exact re-run list
-// (stats[0]).
-struct SecondChanceLDS {
-    float w_key[kWideCap], w_apx[kWideCap];
-    int64_t w_lab[kWideCap];
-    float o_key[64];
-    int64_t o_lab[64];
-    int w_n;
-    unsigned w_tau;
-    float s_sk;
-};
-
-template <int NW>
-__device__ __forceinline__ void second_chance_item(const RerankArgs& a, int item,
-                                                   SecondChanceLDS& L) {
-    constexpr int NT = NW * 64;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc;
-    const int n4 = dp / 4;
-    const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
-    {
-        const int64_t q = a.chance_list[item];
-        const QueryBounds B(a, q);
-        // the same prefix limit as the first pass, from the merged candidates' k-th key
-        const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
-        const float thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
-        if (t == 0) {
-            L.w_n = 0;
-            L.w_tau = key_bits_ordered(INFINITY);
-            L.s_sk = -INFINITY;
-        }
-        if (t < 64) L.o_lab[t] = -1;
-        __syncthreads();
-        const float* rd = a.raw_d + q * a.raw_stride_q;
-        const int64_t* ri = a.raw_i + q * a.raw_stride_q;
-        const int km = a.raw_km, ne = a.raw_lists * km;
-        for (int l = t; l < a.raw_lists; l += NT) {
-            const int e = l * km + km - 1;
-            if (ri[e] >= 0) atomicMin(&L.w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
-        }
-        for (int e = t; e < ne; e += NT) {
-            const int64_t l = ri[e];
-            const float v = rd[e];
-            if (l >= 0 && v <= thr) {
-                const int s = atomicAdd(&L.w_n, 1);
-                if (s < kWideCap) { L.w_apx[s] = v; L.w_lab[s] = l; }
-            }
-        }
-        __syncthreads();
-        const int n = L.w_n;
-        bool ok = n <= kWideCap;
-        if (ok) {
-            const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
-            for (int c0 = wave; c0 < n; c0 += NW * kRerankRows) {
-                const float4* r4[kRerankRows];
-                float acc[kRerankRows];
-#pragma unroll
-                for (int v = 0; v < kRerankRows; ++v)
-                    r4[v] = reinterpret_cast<const float4*>(
-                        a.xb + (L.w_lab[min(c0 + NW * v, n - 1)] - a.id_offset) * dp);
-                rerank_dots<0>(q4, none, n4, lane, r4, acc);
-#pragma unroll
-                for (int v = 0; v < kRerankRows; ++v) {
-                    const int c = c0 + NW * v;
-                    if (lane == 0 && c < n)
-                        L.w_key[c] = rerank_key(acc[v], B.qn, a.xn[L.w_lab[c] - a.id_offset], metric);
-                }
-            }
-            __syncthreads();
-            // rank of every reranked entry by (key, label): labels are distinct (a row sits in
-            // one list)
-            for (int s = t; s < n; s += NT) {
-                const float kv = L.w_key[s];
-                const int64_t lb = L.w_lab[s];
-                int rank = 0;
-                for (int j = 0; j < n && rank < k; ++j)
-                    rank += ranks_before_r(L.w_key[j], L.w_lab[j], kv, lb) ? 1 : 0;
-                if (rank < k) {
-                    L.o_key[rank] = kv;
-                    L.o_lab[rank] = lb;
-                    if (rank == k - 1) L.s_sk = kv;
-                }
-                const float r = fabsf(L.w_apx[s] - kv) /
-                                (B.bound_a(L.w_apx[s]) + B.bound_f(kv) + B.trunc(L.w_apx[s]));
-                atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), __float_as_uint(r));
-            }
-            __syncthreads();
-            // +inf floor: no list dropped a row, so every row was a candidate and W holds all
-            // that can matter
-            const float tauL = key_from_ordered(L.w_tau);
-            ok = tauL == INFINITY || (tauL - B.bound_a(tauL)) > (L.s_sk + B.bound_f(L.s_sk));
-        }
-        if (ok) {
-            if (t < k) {
-                const int64_t lb = L.o_lab[t];
-                a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
-                                        : ((metric == 1) ? L.o_key[t] : -L.o_key[t]);
-                a.I[q * k + t] = lb;
-            }
-        } else if (t == 0) {
-            a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
-        }
-        __syncthreads();                // LDS reused by the next item
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Cross-workgroup hand-off (MI355X_MICROARCH.md "Valid forms"): producer = every storing wave's
 // vmcnt(0) wait, the workgroup barrier, then ONE lane's agent-scope release and counter add;
 // consumer = that lane's agent-scope acquire after the counter says so, vmcnt(0), then the
@@ -267,6 +156,210 @@ __device__ __forceinline__ void grid_barrier(int* ctr, int nwg) {
         lane0_acquire();
     }
     __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Second chance for a query the rerank could not certify (item `item` of chance_list): every
+// entry of the candidate pass's per-split lists with approximate key <= the prefix limit (those
+// above it cannot reach the top k) is reranked, and the certificate is re-run against the list
+// floor alone — the smallest last key of a full list, below which no row outside all lists can
+// be.  A query it cannot settle goes to the exact re-run list (stats[0]).
+//
+// The item is cut into a.sc_slices slices (lists slice, slice + S, ...) that different
+// workgroups rerank at once — a one-query search's second chance is a few hundred dependent row
+// loads, ~350 us in one 2-wave workgroup, ~10 us spread over the grid.  A slice keeps its k best
+// exact (key, label) in the item's workspace and folds its list floor into the item's atomic
+// minimum; the workgroup that completes the item's last slice ranks the S x k survivors (the
+// item's k best are among them), checks the certificate, writes the answer and resets the
+// item's counters.  NW waves per workgroup.
+struct SecondChanceLDS {
+    float w_key[kWideCap], w_apx[kWideCap];
+    int64_t w_lab[kWideCap];
+    float o_key[64];
+    int64_t o_lab[64];
+    int w_n;
+    unsigned w_tau;
+    unsigned s_ratio;
+    float s_sk;
+    int s_last;
+    int s_flag;
+};
+
+// agent-scope relaxed store (global_store ... sc1): written through to where every XCD reads it
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NW>
+__device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int item, int slice,
+                                                    SecondChanceLDS& L) {
+    constexpr int NT = NW * 64;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc, S = a.sc_slices;
+    const int n4 = dp / 4;
+    const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
+    const int64_t q = a.chance_list[item];
+    const QueryBounds B(a, q);
+    // the same prefix limit as the first pass, from the merged candidates' k-th key
+    const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
+    const float thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
+    if (t == 0) {
+        L.w_n = 0;
+        L.w_tau = 0xffffffffu;
+        L.s_ratio = 0u;
+    }
+    __syncthreads();
+    const float* rd = a.raw_d + q * a.raw_stride_q;
+    const int64_t* ri = a.raw_i + q * a.raw_stride_q;
+    const int km = a.raw_km;
+    const int nl = (a.raw_lists - slice + S - 1) / S;          // lists slice, slice + S, ...
+    for (int j = t; j < nl; j += NT) {
+        const int e = (slice + j * S) * km + km - 1;
+        if (ri[e] >= 0) atomicMin(&L.w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
+    }
+    for (int j = t; j < nl * km; j += NT) {
+        const int e = (slice + (j / km) * S) * km + j % km;
+        const int64_t l = ri[e];
+        const float v = rd[e];
+        if (l >= 0 && v <= thr) {
+            const int s2 = atomicAdd(&L.w_n, 1);
+            if (s2 < kWideCap) { L.w_apx[s2] = v; L.w_lab[s2] = l; }
+        }
+    }
+    __syncthreads();
+    const int n = L.w_n;
+    const bool overflow = n > kWideCap;
+    float* const ok_ = a.sc_key + ((int64_t)item * S + slice) * k;
+    int64_t* const ol_ = a.sc_lab + ((int64_t)item * S + slice) * k;
+    if (!overflow) {
+        const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
+        for (int c0 = wave; c0 < n; c0 += NW * kRerankRows) {
+            const float4* r4[kRerankRows];
+            float acc[kRerankRows];
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v)
+                r4[v] = reinterpret_cast<const float4*>(
+                    a.xb + (L.w_lab[min(c0 + NW * v, n - 1)] - a.id_offset) * dp);
+            rerank_dots<0>(q4, none, n4, lane, r4, acc);
+#pragma unroll
+            for (int v = 0; v < kRerankRows; ++v) {
+                const int c = c0 + NW * v;
+                if (lane == 0 && c < n)
+                    L.w_key[c] = rerank_key(acc[v], B.qn, a.xn[L.w_lab[c] - a.id_offset], metric);
+            }
+        }
+        __syncthreads();
+        // this slice's k best by (key, label) (labels are distinct: a row sits in one list);
+        // the observed error / bound goes to the chunk's maximum once per workgroup (one
+        // same-address global atomic per reranked entry serialised the slices: ~100 us)
+        float rmax = 0.f;
+        for (int s2 = t; s2 < n; s2 += NT) {
+            const float kv = L.w_key[s2];
+            const int64_t lb = L.w_lab[s2];
+            int rank = 0;
+            for (int j = 0; j < n && rank < k; ++j)
+                rank += ranks_before_r(L.w_key[j], L.w_lab[j], kv, lb) ? 1 : 0;
+            if (rank < k) { st_sc1(ok_ + rank, kv); st_sc1(ol_ + rank, lb); }
+            rmax = fmaxf(rmax, fabsf(L.w_apx[s2] - kv) /
+                                   (B.bound_a(L.w_apx[s2]) + B.bound_f(kv) + B.trunc(L.w_apx[s2])));
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, off, 64));
+        if (lane == 0) atomicMax(&L.s_ratio, __float_as_uint(rmax));
+    }
+    for (int r = t; r < k; r += NT)
+        if (overflow || r >= n) { st_sc1(ok_ + r, INFINITY); st_sc1(ol_ + r, (int64_t)-1); }
+    __syncthreads();                                    // L.s_ratio complete
+    if (t == 0) {                                       // the slice's floor, error ratio, overflow
+        unsigned* meta = a.sc_meta + ((int64_t)item * S + slice) * 4;
+        st_sc1(meta, L.w_tau);
+        st_sc1(meta + 1, L.s_ratio);
+        st_sc1(meta + 2, overflow ? 1u : 0u);
+    }
+    // Hand-off without an L2 write-back (MI355X_MICROARCH.md, valid forms, table row 1): the
+    // slice lists are stored sc1, every storing wave waits for its stores, then ONE lane adds to
+    // the item's counter; the workgroup whose add comes last reads them with sc1 loads only (an
+    // agent release per slice — buffer_wbl2 of the XCD's L2 — made the slices' completions
+    // serialise: ~5 us per slice).  ONE same-address atomic per slice: the slice's floor, error
+    // ratio and overflow go to its own meta slot (three agent atomics per slice on per-item
+    // words — and one more on the chunk's ratio — cost ~2 us per slice, serialised).
+    wg_release_stores();
+    if (t == 0)
+        L.s_last = __hip_atomic_fetch_add(a.sc_done + item, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+    __syncthreads();
+    const bool last = L.s_last != 0;
+    __syncthreads();                                    // L reused below / by the next slice
+    if (!last) return false;
+
+    // ---- the item's last slice: merge the S sorted slice lists (k each) in one wave — k rounds
+    // of a wave u64 minimum over the S list heads, (ordered key bits | split-local label)
+    // (a quadratic rank of the S x k survivors cost ~80 us at S = 32), certify, answer
+    const float* sk_ = a.sc_key + (int64_t)item * S * k;
+    const int64_t* sl_ = a.sc_lab + (int64_t)item * S * k;
+    if (wave == 0) {
+        auto head = [&](int p) -> uint64_t {
+            if (lane >= S || p >= k) return ~0ull;
+            const int64_t lb = __hip_atomic_load(sl_ + lane * k + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float kv = __hip_atomic_load(sk_ + lane * k + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return lb < 0 ? ~0ull : ((uint64_t)key_bits_ordered(kv) << 32) | (uint32_t)(lb - a.id_offset);
+        };
+        L.o_key[lane] = INFINITY;                       // rounds after an exhausted merge: empty
+        L.o_lab[lane] = -1;
+        int p = 0;
+        uint64_t h = head(0);
+        float sk = -INFINITY;
+        for (int r = 0; r < k; ++r) {
+            const uint64_t m = wave_min_u64(h);
+            if (lane == 0) {
+                L.o_key[r] = m == ~0ull ? INFINITY : key_from_ordered((uint32_t)(m >> 32));
+                L.o_lab[r] = m == ~0ull ? (int64_t)-1 : (int64_t)(uint32_t)m + a.id_offset;
+            }
+            if (m == ~0ull) break;
+            if (r == k - 1) sk = key_from_ordered((uint32_t)(m >> 32));
+            if (h == m) h = head(++p);                  // unique: a row sits in one list
+        }
+        if (lane == 0) L.s_sk = sk;
+        // the item's floor (min over slices), error ratio (max) and overflow (any)
+        unsigned tb = 0xffffffffu, rb = 0u, fb = 0u;
+        if (lane < S) {
+            const unsigned* meta = a.sc_meta + ((int64_t)item * S + lane) * 4;
+            tb = __hip_atomic_load(meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rb = __hip_atomic_load(meta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fb = __hip_atomic_load(meta + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            tb = min(tb, (unsigned)__shfl_xor((int)tb, off, 64));
+            rb = max(rb, (unsigned)__shfl_xor((int)rb, off, 64));
+            fb |= (unsigned)__shfl_xor((int)fb, off, 64);
+        }
+        if (lane == 0) {
+            L.w_tau = tb;
+            L.s_flag = (int)fb;
+            if (rb) atomicMax(reinterpret_cast<unsigned*>(a.stats + 1), rb);
+        }
+    }
+    __syncthreads();
+    const unsigned tb = L.w_tau;
+    const int flag = L.s_flag;
+    // +inf floor: no list dropped a row, so every row was a candidate and the slices hold all
+    // that can matter
+    const float tauL = tb == 0xffffffffu ? INFINITY : key_from_ordered(tb);
+    const bool ok = flag == 0 && (tauL == INFINITY || (tauL - B.bound_a(tauL)) > (L.s_sk + B.bound_f(L.s_sk)));
+    if (ok) {
+        if (t < k) {
+            const int64_t lb = L.o_lab[t];
+            a.D[q * k + t] = lb < 0 ? ((metric == 1) ? FLT_MAX : -FLT_MAX)
+                                    : ((metric == 1) ? L.o_key[t] : -L.o_key[t]);
+            a.I[q * k + t] = lb;
+        }
+    } else if (t == 0) {
+        a.fail_list[atomicAdd(a.stats, 1)] = (int)q;
+    }
+    __syncthreads();
+    if (t == 0) a.sc_done[item] = 0;                    // ready for the next search's items
+    return true;
 }
 
 }  // namespace imgrec

@@ -130,6 +130,10 @@ struct knn_index {
     int64_t* cand2_i = nullptr; size_t cand2_i_cap = 0;
     int* fail = nullptr; size_t fail_cap = 0;          // the uncertified queries of a chunk
     int* chance = nullptr; size_t chance_cap = 0;      // the second-chance queue of a chunk
+    float* sc_key = nullptr; size_t sc_key_cap = 0;    // sliced second chance (RerankArgs::sc_*)
+    int64_t* sc_lab = nullptr; size_t sc_lab_cap = 0;
+    unsigned* sc_meta = nullptr; size_t sc_meta_cap = 0;
+    int* sc_done = nullptr; size_t sc_done_cap = 0;
     int* stat = nullptr;                               // 12 ints: two chunk parities + totals
     int stat_seq = 0;                                  // chunks run (parity = seq & 1)
     bool stat_valid = false;                           // the last search ran a candidate path

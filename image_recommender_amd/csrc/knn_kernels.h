@@ -79,6 +79,16 @@ struct RerankArgs {
     int raw_lists = 0, raw_km = 0;
     int64_t raw_stride_q = 0;
     int* tail_ctl = nullptr;    // the certificate tail's grid-barrier counters (zeroed by the rerank)
+    // second chance in slices (cert_tail_kernel): item i's raw lists are cut into sc_slices
+    // slices reranked by different workgroups; per slice its k best (key, label) at
+    // sc_key / sc_lab[(i * sc_slices + s) * k] and (floor bits, error ratio bits, overflow) at
+    // sc_meta[(i * sc_slices + s) * 4]; per item the completed-slice count (reset by the item's
+    // last slice; allocated zero)
+    int sc_slices = 1;
+    float* sc_key = nullptr;
+    int64_t* sc_lab = nullptr;
+    unsigned* sc_meta = nullptr;
+    int* sc_done = nullptr;
 };
 
 // The certificate tail of a candidate chunk (knn_kernels.hip cert_tail_kernel), ONE launch after

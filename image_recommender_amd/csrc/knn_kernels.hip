@@ -669,8 +669,9 @@ __device__ __forceinline__ void merge_query_wave(const float* __restrict__ cd,
 // Otherwise, with no workgroup ever waiting on one that has not yet claimed work (so the launch
 // cannot deadlock whatever else shares the GPU — the multi-device index runs shards concurrently
 // on one device):
-//   1. second-chance items are claimed from ctl[0], completions counted in ctl[1]; the workgroup
-//      that completes the last one (or takes ticket 0 when none was queued) is the planner;
+//   1. second-chance units (item, slice) are claimed from ctl[0]; the workgroup that finishes an
+//      item's last slice answers it and counts it in ctl[1]; the one that completes the last item
+//      (or takes ticket 0 when none was queued) is the planner;
 //   2. the planner folds the stats, gathers the uncertified queries (fail_list) into fq / fqn
 //      (zero rows up to a multiple of 32), zeroes the per-query-block tickets and publishes
 //      ctl[2] = 1; everyone else waits for it (the planner is running: it completed an item);
@@ -707,13 +708,18 @@ cert_tail_kernel(const TailArgs a) {
     // ---- 1. second chance ----------------------------------------------------------------
     bool planner = false;
     if (n_chance > 0) {
+        // units = (item, slice), claimed from ctl[0]; the workgroup that finishes an item's last
+        // slice counts the item in ctl[1]
+        const int S = a.r.sc_slices;
         for (;;) {
             if (t == 0) s_val = __hip_atomic_fetch_add(ctl + 0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
-            const int item = s_val;
+            const int unit = s_val;
             __syncthreads();
-            if (item >= n_chance) break;
-            second_chance_item<kTailWaves>(a.r, item, *reinterpret_cast<SecondChanceLDS*>(smem));
+            if (unit >= n_chance * S) break;
+            const bool finished = second_chance_slice<kTailWaves>(a.r, unit / S, unit % S,
+                                                                  *reinterpret_cast<SecondChanceLDS*>(smem));
+            if (!finished) continue;
             wg_release_stores();
             if (t == 0) {
                 const int done = lane0_release_add(ctl + 1);

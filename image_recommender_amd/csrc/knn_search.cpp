@@ -115,6 +115,24 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     r.stats = ix->stat + 4 * parity;
     r.fail_list = ix->fail;
     r.chance_list = ix->chance;
+    if (r.raw_d) {
+        // sliced second chance: up to 64 slices per item (profiles/r03/second_chance/)
+        static const int kSlices = [] {           // IMGREC_SC_SLICES overrides (measurements)
+            const char* e = std::getenv("IMGREC_SC_SLICES");
+            const int v = e ? std::atoi(e) : 0;
+            return v > 0 ? v : 64;
+        }();
+        r.sc_slices = std::max(1, std::min({kSlices, r.raw_lists, 1024 / k}));
+        const size_t ns = (size_t)nq * r.sc_slices * k;
+        if ((rc = grow(&ix->sc_key, &ix->sc_key_cap, ns)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->sc_lab, &ix->sc_lab_cap, ns)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->sc_meta, &ix->sc_meta_cap, (size_t)nq * r.sc_slices * 4)) != KNN_OK) return rc;
+        const size_t c0 = ix->sc_done_cap;
+        if ((rc = grow(&ix->sc_done, &ix->sc_done_cap, (size_t)nq)) != KNN_OK) return rc;
+        if (ix->sc_done_cap != c0)      // (re)allocated: the self-resetting counters start at 0
+            KNN_HIP(hipMemsetAsync(ix->sc_done, 0, ix->sc_done_cap * sizeof(int), st));
+        r.sc_key = ix->sc_key; r.sc_lab = ix->sc_lab; r.sc_meta = ix->sc_meta; r.sc_done = ix->sc_done;
+    }
     r.tail_ctl = ix->tail_ctl;
     KNN_HIP(launch_rerank_certify(r, st));
     TailArgs t{};
