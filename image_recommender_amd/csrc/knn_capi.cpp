@@ -232,7 +232,8 @@ int create_single(int d, int metric, int device, knn_index** out) {
 void free_single(knn_index* ix) {
     DeviceGuard g(ix->device);
     (void)hipDeviceSynchronize();       // searches on other streams may still use the buffers
-    for (void* p : {(void*)ix->x8, (void*)ix->x8s, (void*)ix->x8r, (void*)ix->x8r_max})
+    for (void* p : {(void*)ix->x8, (void*)ix->x8s, (void*)ix->x8r, (void*)ix->x8r_max,
+                    (void*)ix->q8, (void*)ix->q8s, (void*)ix->q8r})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->pq, (void*)ix->pd, (void*)ix->pi})
         if (p) (void)hipHostFree(p);
@@ -599,7 +600,7 @@ int knn_plan_kernel(const knn_index_t* cix, int64_t nq, int k, char* name, int c
     const int l2 = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     if (use_i8(ix, cn, k)) {
         const Plan p = make_i8_plan(ix->ntotal, cn, k, ix->cus);
-        std::snprintf(name, cap, "knn_i8_scan_kernel<%d, %d, %d>", cn <= 2 ? (int)cn : 4, p.km,
+        std::snprintf(name, cap, "knn_i8_scan_kernel<%d, %d, %d>", cn <= 2 ? (int)cn : (cn <= 4 ? 4 : 8), p.km,
                       (ix->nblk8 + 15) / 16);
     } else if (use_b16(ix, cn, k)) {
         const Plan p = make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb);

@@ -39,7 +39,8 @@ struct QueryBounds {
         //   bf16:  |q.(x - xh) + (q - qh).xh| + accumulation <= |q| R + dq (X + R) + c_acc |qh| |xh|
         //          (Cauchy-Schwarz with the stored residual norms; R = max row residual, X = max
         //          |x|, |qh| <= |q| + dq, |xh| <= X + R), inflated for the bound's fp32 evaluation
-        //   i8:    the same with dq = 0 (the query stays fp32) and R the int8 copy's residual
+        //   i8:    the same with dq = |q - q~| of the two-level int8 query (q8r) and R the int8
+        //          copy's residual
         if (a.mode == kModeBF16 || a.mode == kModeI8) {
             const float sq = sqrtf(qn), X = sqrtf(xm), R = *a.xr_max;
             const float dq = a.q_resid ? a.q_resid[q] : 0.f;

@@ -1,28 +1,31 @@
 // knn_i8.hip — the small-batch candidate pass on a block-scaled int8 copy of the corpus (gfx950).
 //
-// A search of one or two queries (the reference CLI's regime: main/search_from_image.py:247
+// A search of a few queries (the reference CLI's regime: main/search_from_image.py:247
 // searches ONE query vector per call) is HBM-bound: the bf16 candidate pass streams 2 bytes per
 // element (3.97 GB at 1M x 1968; 0.646 ms at 6.1 TB/s, profiles/r03/nq1_final.jsonl).  This pass
-// streams 1 byte per element plus one fp32 scale per 64 (2.1 GB) and keeps the same contract as
+// streams 1 byte per element plus one fp32 scale per 64 (2.17 GB) and keeps the same contract as
 // the bf16 pass: per (query, row split) the KM best APPROXIMATE keys, which the candidate merge,
 // the fp32 rerank and the certificate (knn_refine.hip, knn_certify.h kModeI8) turn into the exact
 // answer.  The approximation is certified, not trusted:
 //
 //   x~ = s_b * c   per 64-element block b, s_b = max|x_b| / 127, c = rint(x / s_b) in [-127, 127]
-//   |q.x - q.x~| <= |q| |x - x~| <= |q| R           (R = max stored residual norm)
+//   q~ = s_hi c_hi + s_lo c_lo   two levels of the same per query block (|q - q~| ~ 2^-14 |q|)
+//   |q.x - q~.x~| <= |q| |x - x~| + |q - q~| |x~|     (R = max stored residual norm of the rows)
 //
-// and the query stays fp32 (no query rounding term).  On the bench rows (1M x 1968, unit-norm
-// parts) R = 0.016 against the bf16 copy's 0.0036; the rows within the certificate's band of the
-// 10th approximate key number 21-53 per query (numpy over the whole 1M corpus, DESIGN.md
-// "Small batches"), below the rerank's 64 candidates.
+// On the bench rows (1M x 1968, unit-norm parts) R = 0.016 against the bf16 copy's 0.0036; the
+// rows within the certificate's band of the 10th approximate key number 21-53 per query (numpy
+// over the whole 1M corpus, tools/i8_band_check.py), below the rerank's 64 candidates.
 //
 // Scan: one workgroup per row split (8-row groups s, s + nsplit, ... as the bf16 kernels, so a
 // store with similar images on adjacent rows spreads them over every split), four waves; a wave
 // takes one 8-row group at a time, a 16-lane group per row, lane j the 64-element blocks j,
-// j + 16, ... of its row: 16-B code loads, the query from LDS in fp32, int8 -> fp32 by the SDWA
-// byte-select convert, FMA chains per 16-element chunk, the block scale, a DPP row-rotate sum over
-// the 16 lanes.  Lane j (< NQ) of each group keeps query j's list; at the end the 16 lists of a
-// split are merged in LDS to one list of KM.
+// j + 16, ... of its row: 16-B code loads (two register sets: the next group's loads in flight),
+// the query's codes from LDS, exact int32 v_dot4_i32_i8 products of the row's codes with the
+// query's hi and lo codes (no int8 -> fp32 conversions: 0.56 VALU instructions per element and
+// query, against 2 for an fp32 FMA form that converts every code), one fp32 fold per block
+// (acc += s_x (s_hi D_hi + s_lo D_lo)), a DPP row-rotate sum over the 16 lanes.  Lane j (< NQ)
+// of each row group keeps query j's list; at the end the 16 lists of a split are merged in LDS
+// to one list of KM.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -107,6 +110,65 @@ i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t
     if (lane == 0) resid[row] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
 }
 
+// Query side: two-level int8 codes per 64-element block, q~ = s_hi c_hi + s_lo c_lo
+// (c_hi = rint(q / s_hi), s_hi = max|q_b| / 127; c_lo the same of q - s_hi c_hi), so the scan's
+// products are exact int32 dot4s and the query's own rounding |q - q~| (about 2^-14 |q|) is
+// the certificate's dq term (q_resid).  One wave per query, lane b = block b (nblk <= 64);
+// out: codes[q][b] = 64 hi | 64 lo, scales[q][b] = (s_hi, s_lo), resid[q] (inflated for its own
+// fp32 evaluation as the rows' is).
+__global__ void __launch_bounds__(64)
+i8_query_kernel(const float* __restrict__ qp, int dp, int nblk, int8_t* __restrict__ codes,
+                float* __restrict__ scales, float* __restrict__ resid) {
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x;
+    const float* x = qp + q * dp;
+    float rsq = 0.f, xsq = 0.f;
+    if (lane < nblk) {
+        float v[kBlk];
+        float mx = 0.f;
+#pragma unroll
+        for (int e = 0; e < kBlk; ++e) {
+            const int i = lane * kBlk + e;
+            v[e] = i < dp ? x[i] : 0.f;
+            mx = fmaxf(mx, fabsf(v[e]));
+            xsq = fmaf(v[e], v[e], xsq);
+        }
+        uint32_t w[2][kBlk / 4];
+        float sc[2];
+#pragma unroll
+        for (int lev = 0; lev < 2; ++lev) {
+            const float s = mx / 127.f, inv = mx > 0.f ? 127.f / mx : 0.f;
+            float mx2 = 0.f;
+#pragma unroll
+            for (int e4 = 0; e4 < kBlk / 4; ++e4) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int c = max(-127, min(127, (int)rintf(v[4 * e4 + t] * inv)));
+                    v[4 * e4 + t] -= (float)c * s;                 // the residual, next level's input
+                    mx2 = fmaxf(mx2, fabsf(v[4 * e4 + t]));
+                    word |= ((uint32_t)c & 0xffu) << (8 * t);
+                }
+                w[lev][e4] = word;
+            }
+            sc[lev] = s;
+            mx = mx2;
+        }
+#pragma unroll
+        for (int e = 0; e < kBlk; ++e) rsq = fmaf(v[e], v[e], rsq);
+        uint4* dst = reinterpret_cast<uint4*>(codes + (q * nblk + lane) * 2 * kBlk);
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            dst[c] = make_uint4(w[c >> 2][4 * (c & 3)], w[c >> 2][4 * (c & 3) + 1],
+                                w[c >> 2][4 * (c & 3) + 2], w[c >> 2][4 * (c & 3) + 3]);
+        scales[(q * nblk + lane) * 2] = sc[0];
+        scales[(q * nblk + lane) * 2 + 1] = sc[1];
+    }
+    rsq = wave_sum(rsq);
+    xsq = wave_sum(xsq);
+    if (lane == 0) resid[q] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
+}
+
 // Ascending list, labels arriving in increasing order: slot p's key is the median of (kd[p-1], d,
 // kd[p]) (ties keep the earlier, smaller label); d = +inf is a no-op.
 template <int K>
@@ -128,15 +190,16 @@ template <int NQ, int KM, int NBI>
 __global__ void __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2)))
 knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ scales,
                    const float* __restrict__ xnorm, int nrows, int nblk,
-                   const float* __restrict__ qp, const float* __restrict__ qnorm, int nq, int dp,
+                   const int8_t* __restrict__ qcodes, const float* __restrict__ qscales,
+                   const float* __restrict__ qnorm, int nq,
                    int nsplit, int64_t id_offset, int l2, float* __restrict__ cand_d,
                    int64_t* __restrict__ cand_i, int ncand) {
-    // query in LDS, block b at b * kQB floats: the 16-B pad per block puts lane j's block
-    // (b = j + 16 bi) on 16-B bank slot j, so a ds_read_b128 lane group (16 distinct j) is
-    // conflict-free (unpadded, every block started on bank 0: 16-way conflicts)
-    constexpr int kQB = kBlk + 4;
-    constexpr int kQS = 16 * NBI * kQB;                // LDS floats per query (zero padded)
-    __shared__ __attribute__((aligned(16))) float sq[NQ * kQS];
+    // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
+    // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
+    // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
+    constexpr int kQB = 2 * kBlk + 16;
+    __shared__ __attribute__((aligned(16))) int8_t sqc[NQ][16 * NBI][kQB];
+    __shared__ float sqs[NQ][16 * NBI][2];
     __shared__ float fd[NQ][16][KM];
     __shared__ int fi[NQ][16][KM];
 
@@ -144,9 +207,17 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = lane & 15, g = lane >> 4;
     const int64_t rowb = i8_row_bytes(nblk);
-    for (int i = tid; i < NQ * kQS; i += kWaves * 64) {
-        const int qi = i / kQS, r = i - qi * kQS, b = r / kQB, o = r - b * kQB, e = b * kBlk + o;
-        sq[i] = (qi < nq && o < kBlk && e < dp) ? qp[(int64_t)qi * dp + e] : 0.f;
+    for (int i = tid; i < NQ * 16 * NBI * 8; i += kWaves * 64) {          // 16-B chunks
+        const int qi = i / (16 * NBI * 8), r = i - qi * (16 * NBI * 8), b = r >> 3, c = r & 7;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (qi < nq && b < nblk) v = reinterpret_cast<const uint4*>(qcodes + ((int64_t)qi * nblk + b) * 2 * kBlk)[c];
+        *reinterpret_cast<uint4*>(&sqc[qi][b][16 * c]) = v;
+    }
+    for (int i = tid; i < NQ * 16 * NBI; i += kWaves * 64) {
+        const int qi = i / (16 * NBI), b = i - qi * (16 * NBI);
+        const bool in = qi < nq && b < nblk;
+        sqs[qi][b][0] = in ? qscales[((int64_t)qi * nblk + b) * 2] : 0.f;
+        sqs[qi][b][1] = in ? qscales[((int64_t)qi * nblk + b) * 2 + 1] : 0.f;
     }
     float qn[NQ];
 #pragma unroll
@@ -198,37 +269,48 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
 #pragma unroll
         for (int bi = 0; bi < NBI; ++bi) {
             const int b = j + 16 * bi;
+            // exact int32 dots of the row's 64 codes with the query block's hi and lo codes
+            // (|sum| <= 64 * 127^2 < 2^24: exact in fp32 too), folded once per block:
+            // acc += s_x (s_hi D_hi + s_lo D_lo)
+            int dh[2][NQ], dl[2][NQ];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) dh[h][q] = dl[h][q] = 0;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 // chunk by chunk: the laundered offset keeps this chunk's query reads below the
-                // previous chunk's (pinned) accumulators, so at most one chunk's query values and
-                // converted codes are live (the compiler otherwise hoists every chunk's reads:
-                // 4 x NBI x 16 more registers)
-                int qoff = b * kQB + 16 * c;
+                // previous chunk's (pinned) dots, so one chunk's query codes are live at a time
+                int qoff = 16 * c;
                 asm volatile("" : "+v"(qoff));
 #pragma unroll
                 for (int q = 0; q < NQ; ++q) {
-                    const float4* qv4 = reinterpret_cast<const float4*>(sq + q * kQS + qoff);
-                    const float4 qa = qv4[0], qb = qv4[1], qc = qv4[2], qd = qv4[3];
-                    const float qs[16] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w,
-                                          qc.x, qc.y, qc.z, qc.w, qd.x, qd.y, qd.z, qd.w};
+                    const uint4 hi = *reinterpret_cast<const uint4*>(&sqc[q][b][qoff]);
+                    const uint4 lo = *reinterpret_cast<const uint4*>(&sqc[q][b][kBlk + qoff]);
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const uint32_t wv[4] = {G.cw[h][bi][c].x, G.cw[h][bi][c].y, G.cw[h][bi][c].z,
-                                                G.cw[h][bi][c].w};
-                        float p0 = 0.f, p1 = 0.f;            // two 8-term chains per 16-element chunk
-#pragma unroll
-                        for (int t = 0; t < 8; ++t) {
-                            p0 = fmaf(qs[t], (float)(signed char)(wv[t >> 2] >> (8 * (t & 3))), p0);
-                            p1 = fmaf(qs[8 + t], (float)(signed char)(wv[2 + (t >> 2)] >> (8 * (t & 3))), p1);
-                        }
-                        acc[h][q] = fmaf(G.sc[h][bi], p0 + p1, acc[h][q]);
+                        const uint4 w = G.cw[h][bi][c];
+                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.x, (int)hi.x, dh[h][q], false);
+                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.y, (int)hi.y, dh[h][q], false);
+                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.z, (int)hi.z, dh[h][q], false);
+                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.w, (int)hi.w, dh[h][q], false);
+                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.x, (int)lo.x, dl[h][q], false);
+                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.y, (int)lo.y, dl[h][q], false);
+                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.z, (int)lo.z, dl[h][q], false);
+                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.w, (int)lo.w, dl[h][q], false);
                     }
                 }
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
-                    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[h][q]));
+                    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(dh[h][q]), "+v"(dl[h][q]));
+            }
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const float sh = sqs[q][b][0], sl = sqs[q][b][1];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    acc[h][q] = fmaf(G.sc[h][bi], fmaf(sl, (float)dl[h][q], sh * (float)dh[h][q]), acc[h][q]);
             }
         }
         // keys; lane j (< NQ) of the row's group inserts query j's key (rows increase per lane)
@@ -267,8 +349,8 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         }
     }
     __syncthreads();
-    if (wave != 0) return;
-    const int fq = lane >> 4, fl = lane & 15;              // query, list
+    // wave w merges queries 4w .. 4w + 3, a 16-lane group per query, lane = list
+    const int fq = wave * 4 + (lane >> 4), fl = lane & 15;
     if (fq >= NQ || fq >= nq) return;                    // (whole 16-lane groups leave together)
     int pos = 0;
     for (int p = 0; p < KM; ++p) {
@@ -305,13 +387,23 @@ hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* 
     return hipGetLastError();
 }
 
+hipError_t launch_i8_query(const float* qp, int64_t nq, int dp, int nblk, int8_t* codes, float* scales,
+                           float* resid, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (nblk <= 0 || nblk > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(i8_query_kernel, dim3((unsigned)nq), dim3(64), 0, st, qp, dp, nblk, codes,
+                       scales, resid);
+    return hipGetLastError();
+}
+
 hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
     if (a.nblk <= 0 || a.nblk > 64 || a.nq < 1 || a.nsplit < 1) return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);
     const int nbi = (a.nblk + 15) / 16;
 #define IMGREC_I8(NQV, KMV, NBIV)                                                                 \
     hipLaunchKernelGGL((knn_i8_scan_kernel<NQV, KMV, NBIV>), grid, block, 0, st, a.codes, a.scales, \
-                       a.xnorm, a.nrows, a.nblk, a.qp, a.qnorm, a.nq, a.dp, a.nsplit, a.id_offset,  \
+                       a.xnorm, a.nrows, a.nblk, a.qcodes, a.qscales, a.qnorm, a.nq, a.nsplit,      \
+                       a.id_offset,                                                                 \
                        a.l2, a.cand_d, a.cand_i, a.ncand)
 #define IMGREC_I8_NBI(NQV, KMV)                                   \
     do {                                                          \
@@ -331,6 +423,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
     if (a.nq == 1) IMGREC_I8_KM(1);
     else if (a.nq == 2) IMGREC_I8_KM(2);
     else if (a.nq <= 4) IMGREC_I8_KM(4);
+    else if (a.nq <= 8) IMGREC_I8_KM(8);
     else return hipErrorInvalidValue;
 #undef IMGREC_I8_KM
 #undef IMGREC_I8_NBI

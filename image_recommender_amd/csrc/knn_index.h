@@ -82,7 +82,7 @@ float split_coef(int dp);
 float rerank_coef(int dp);
 float b16_acc_coef(int dpb);
 // int8 small-batch pass (knn_i8.hip): batches of at most kI8MaxQ queries, K' = kB16Cand
-constexpr int kI8MaxQ = 4;
+constexpr int kI8MaxQ = 8;
 float i8_acc_coef(int nblk);
 Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus);
 constexpr int kB16Cand = 64;                   // K': candidates the bf16 pass hands to the rerank
@@ -104,6 +104,9 @@ struct knn_index {
     float* x8r = nullptr;    // cap: |x - s c| per row
     float* x8r_max = nullptr; size_t x8r_max_cap = 0;   // device scalar, max of x8r
     int nblk8 = 0;           // 64-element blocks per row (d <= 4096)
+    int8_t* q8 = nullptr; size_t q8_cap = 0;        // a search's two-level query codes
+    float* q8s = nullptr; size_t q8s_cap = 0;       //   their scales
+    float* q8r = nullptr; size_t q8r_cap = 0;       //   |q - q~| per query
     float* xn_max = nullptr; // device scalar, max |x|^2 (refreshed when rows change)
     float* xr_max = nullptr; // device scalar, max |x - bf16(x)|
     int dpb = 0;             // bf16 row stride (elements)

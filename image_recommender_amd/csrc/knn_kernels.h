@@ -167,15 +167,16 @@ constexpr int kB16PackMaxIB = IMGREC_B16_PACK_MAXIB;
 constexpr int kB16BigRows = 256, kB16BigQueries = 256, kB16BigMinQ = IMGREC_B16_BIG_MINQ;
 
 // Small-batch candidate pass on the block-scaled int8 copy (knn_i8.hip): per (query, row split)
-// the km best approximate keys, nq <= 4 queries in one launch, nsplit workgroups.
+// the km best approximate keys, nq <= 8 queries in one launch, nsplit workgroups.
 struct I8Args {
     const int8_t* codes;        // cap x nblk*64 codes
     const float* scales;        // cap x nblk block scales
     const float* xnorm;         // |x|^2 per stored row (exact)
     int nrows, nblk;
-    const float* qp;            // fp32 queries, nq x dp
+    const int8_t* qcodes;       // nq x nblk x (64 hi | 64 lo) two-level query codes
+    const float* qscales;       // nq x nblk x (s_hi, s_lo)
     const float* qnorm;
-    int nq, dp, km, nsplit, l2;
+    int nq, km, nsplit, l2;
     int64_t id_offset;
     float* cand_d;              // nq x ncand keys, one sorted list of km per split
     int64_t* cand_i;
@@ -187,6 +188,9 @@ __host__ __device__ inline int64_t i8_row_bytes(int nblk) { return (int64_t)1024
 hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* codes, float* scales,
                           float* resid, hipStream_t st);
 hipError_t launch_i8_scan(const I8Args& a, hipStream_t st);
+// fp32 queries (stride dp) -> two-level int8 block codes + scales + |q - q~| per query
+hipError_t launch_i8_query(const float* qp, int64_t nq, int dp, int nblk, int8_t* codes, float* scales,
+                           float* resid, hipStream_t st);
 
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);

@@ -79,11 +79,11 @@ float rerank_coef(int dp) {
 float b16_acc_coef(int dpb) {
     return (float)(1.02 * (5.0 * (dpb / 16) + 16.0) * std::ldexp(1.0, -23));
 }
-// int8 small-batch pass (knn_i8.hip): per lane, two 8-term fp32 FMA chains per 16-element chunk
-// and their sum, the block scale folded into the lane's accumulator by one FMA per chunk (4 chunks
-// x ceil(nblk/16) blocks), then the 16-lane DPP sum: 1.02 * gamma_n with
-// n = 8 + 1 + 4 ceil(nblk/16) + 4 (+ 3 slack), relative to |q| |x~| (the codes and scales are
-// exact in fp32; the query is not rounded).  Unit roundoff 2^-23 as above.
+// int8 small-batch pass (knn_i8.hip): per block an exact int32 dot of the row's and the query's
+// codes per level (exact in fp32 as well, |D| < 2^24), the fold s_x (s_hi D_hi + s_lo D_lo) into
+// the lane's accumulator (three roundings), ceil(nblk/16) blocks per lane, then the 16-lane DPP
+// sum: gamma_n with n = 3 + ceil(nblk/16) + 4 — bounded here, generously, by
+// 1.02 * (16 + 4 ceil(nblk/16)) u, u = 2^-23, relative to (|q| + dq)(|x~|) as the bf16 one.
 float i8_acc_coef(int nblk) {
     return (float)(1.02 * (16.0 + 4.0 * ((nblk + 15) / 16)) * std::ldexp(1.0, -23));
 }

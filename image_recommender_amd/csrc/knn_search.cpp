@@ -243,7 +243,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
 }
 
-// Block-scaled int8 candidates (fp32 VALU dot, batches of <= kI8MaxQ queries) + exact fp32
+// Block-scaled int8 candidates (int8 dot4 products, batches of <= kI8MaxQ queries) + exact fp32
 // rerank of K' = 64 + certificate: the bf16 path's chain with the int8 copy's bound.
 int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
              int64_t* I, hipStream_t st, bool timed, bool first) {
@@ -259,9 +259,14 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
     if ((rc = grow_stats(ix, nq, st)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->q8, &ix->q8_cap, (size_t)nq * ix->nblk8 * 128)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->q8s, &ix->q8s_cap, (size_t)nq * ix->nblk8 * 2)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->q8r, &ix->q8r_cap, (size_t)nq)) != KNN_OK) return rc;
+    KNN_HIP(launch_i8_query(qpad, nq, ix->dp, ix->nblk8, ix->q8, ix->q8s, ix->q8r, st));
     I8Args a{};
     a.codes = ix->x8; a.scales = ix->x8s; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
-    a.nblk = ix->nblk8; a.qp = qpad; a.qnorm = qnorm; a.nq = (int)nq; a.dp = ix->dp; a.km = p.km;
+    a.nblk = ix->nblk8; a.qcodes = ix->q8; a.qscales = ix->q8s; a.qnorm = qnorm; a.nq = (int)nq;
+    a.km = p.km;
     a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
     a.cand_i = ix->cand_i; a.ncand = p.ncand;
     hipEvent_t e1 = nullptr;
@@ -284,7 +289,7 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = i8_acc_coef(ix->nblk8);
     r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
     r.c_trunc = 0.f;
-    r.q_resid = nullptr; r.xr_max = ix->x8r_max; r.floor = ix->floor;
+    r.q_resid = ix->q8r; r.xr_max = ix->x8r_max; r.floor = ix->floor;
     r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = p.km;
     r.raw_stride_q = p.ncand;
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
@@ -347,8 +352,9 @@ bool use_b16(const knn_index* ix, int64_t nq, int k) {
 }
 
 // AUTO: batches of <= kI8AutoQ queries on an index the bf16 path would serve as small (the int8
-// copy streams about half of the bf16 copy's bytes; its VALU dot costs grow with the batch)
-constexpr int kI8AutoQ = 2;
+// copy streams about half of the bf16 copy's bytes; the scan's LDS query reads grow with the
+// batch: nq <= 4 stays HBM-bound, nq = 5-8 is LDS-bound and slower than the bf16 pass)
+constexpr int kI8AutoQ = 4;
 bool use_i8(const knn_index* ix, int64_t nq, int k) {
     if (ix->nblk8 <= 0 || k > KNN_MAX_K || nq > kI8MaxQ) return false;
     if (ix->mode == KNN_SEARCH_I8) return true;

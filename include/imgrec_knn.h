@@ -90,14 +90,14 @@ enum knn_error {
  *       queries on an index of >= 16384 rows and for smaller batches on an index of >= 131072
  *       rows (the bf16 copy streams half the bytes); the split path when bf16 is unavailable and
  *       the batch is large; everything else the exact fp32 kernel.
- *       Batches of <= 2 queries (the reference CLI's one-query searches) on such an index take
+ *       Batches of <= 4 queries (the reference CLI's one-query searches) on such an index take
  *       the int8 path instead: a block-scaled int8 copy of the rows (one fp32 scale per 64
- *       elements, about half the bf16 copy's bytes, built on the first such search), an fp32
- *       query and an fp32 VALU dot product, K' = 64, the same certificate with the int8 copy's
- *       residual bound (csrc/knn_i8.hip).
+ *       elements, about half the bf16 copy's bytes, built on the first such search), a
+ *       two-level int8 query and exact int32 dot4 products, K' = 64, the same certificate with
+ *       the int8 copy's and the query's residual bounds (csrc/knn_i8.hip).
  * EXACT: always the fp32 kernel.  SPLIT: the split path (bf16 hi/lo, three MFMAs per product,
  *       K' = 16/32) whenever k <= 16 and d >= 256.  BF16: the bf16 path for every batch (tests).
- * I8:   the int8 path for batches of <= 4 queries (64 <= d <= 4096; tests), else as AUTO. */
+ * I8:   the int8 path for batches of <= 8 queries (64 <= d <= 4096; tests), else as AUTO. */
 enum knn_search_mode {
     KNN_SEARCH_AUTO = 0,
     KNN_SEARCH_EXACT = 1,

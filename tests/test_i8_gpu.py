@@ -1,8 +1,8 @@
 """Parity tests of the int8 small-batch candidate path (include/imgrec_knn.h KNN_SEARCH_I8, the AUTO
-default for batches of <= 2 queries on an index of >= 131072 rows; csrc/knn_i8.hip).
+default for batches of <= 4 queries on an index of >= 131072 rows; csrc/knn_i8.hip).
 
-The int8 path scores rows on a block-scaled int8 copy (one fp32 scale per 64 elements) with an
-fp32 query, reranks K' = 64 candidates in exact fp32 and certifies per query, from the stored
+The int8 path scores rows on a block-scaled int8 copy (one fp32 scale per 64 elements) with a
+two-level int8 query (exact int32 dot4 products), reranks K' = 64 candidates in exact fp32 and certifies per query, from the stored
 residual norms |x - s c|, that no row outside the candidates can rank before a returned one;
 uncertified queries get the second chance over the per-split lists, then the exact re-run.  The
 results must satisfy the SAME contract as the exact path (tests/knn_check.py against the float64
@@ -99,15 +99,15 @@ def test_i8_concat_layout_self_query(faiss):
 
 
 def test_i8_auto_picks_int8_for_single_queries(faiss):
-    """AUTO: one or two queries on >= 131072 rows take the int8 path, three take the bf16 path."""
+    """AUTO: one to four queries on >= 131072 rows take the int8 path, five take the bf16 path."""
     d = 256
     xb = mixture(140000, d, centres=200, seed=3)
-    xq = mixture(3, d, centres=200, seed=4)
+    xq = mixture(5, d, centres=200, seed=4)
     idx = faiss.IndexFlatL2(d)
     idx.add(xb)
     from oracle.flat_knn import search_exact
     orc = search_exact(xb, xq, 11, "l2")
-    for nq, path in ((1, 3), (2, 3), (3, 2)):
+    for nq, path in ((1, 3), (2, 3), (3, 3), (4, 3), (5, 2)):
         D, I = idx.search(xq[:nq], 10)
         assert _lib().knn_last_path(idx.handle) == path
         check_knn(D, I, xb, xq[:nq], 10, "l2", min_exact_frac=0.5,
@@ -172,7 +172,22 @@ def test_i8_clustered_storage(faiss):
     check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
 
 
-def test_i8_mode_batch_above_four_served_as_auto(faiss):
+@pytest.mark.parametrize("nq", [5, 6, 8])
+@pytest.mark.parametrize("metric", ["l2", "cosine"])
+def test_i8_batches_of_five_to_eight(faiss, nq, metric):
+    """The NQ = 8 scan instance (search_mode "i8" only): every query's 16 lists are folded."""
+    xb = mixture(12001, 300, centres=60, seed=nq)
+    xq = mixture(nq, 300, centres=60, seed=nq + 50)
+    idx = _index(faiss, 300, metric)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, 12)
+    assert _lib().knn_last_path(idx.handle) == 3
+    _stats(idx, nq)
+    check_knn(D, I, xb, xq, 12, metric, min_exact_frac=0.5)
+
+
+def test_i8_mode_batch_above_eight_served_as_auto(faiss):
     xb = mixture(5000, 128, centres=20, seed=1)
     xq = mixture(40, 128, centres=20, seed=2)
     idx = faiss.IndexFlatL2(128)

@@ -69,7 +69,7 @@ def test_random_case_matches_oracle(faiss, n, d, nq, k, metric, mode, adds, seed
 
 
 def _i8_cases(n_cases=24, seed=2027):
-    """The int8 small-batch path (search_mode "i8", knn_i8.hip): batches of 1-4 queries (and 5, 40:
+    """The int8 small-batch path (search_mode "i8", knn_i8.hip): batches of 1-5 queries (and 40:
     served as AUTO), tiny and ragged corpora, d below the path's 64 (refused at the setter), k past
     the fused lists (the large-k path takes it)."""
     rng = np.random.default_rng(seed)
