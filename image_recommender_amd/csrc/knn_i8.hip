@@ -197,11 +197,18 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
     // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
     // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
+    // (the final fold's lists reuse the codes' LDS: 39 KB instead of 55 KB per workgroup at NQ = 8
+    // keeps three workgroups on a CU)
     constexpr int kQB = 2 * kBlk + 16;
-    __shared__ __attribute__((aligned(16))) int8_t sqc[NQ][16 * NBI][kQB];
+    union Lds {
+        int8_t qc[NQ][16 * NBI][kQB];
+        struct { float d[NQ][16][KM]; int i[NQ][16][KM]; } f;
+    };
+    __shared__ __attribute__((aligned(16))) Lds lds;
+    auto& sqc = lds.qc;
+    auto& fd = lds.f.d;
+    auto& fi = lds.f.i;
     __shared__ float sqs[NQ][16 * NBI][2];
-    __shared__ float fd[NQ][16][KM];
-    __shared__ int fi[NQ][16][KM];
 
     const int split = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -231,21 +238,27 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     const bool owner = j < NQ && j < nq;
 
     const int ngroups = (nrows + kGroup - 1) / kGroup;
-    const int cnt = split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0;
+    // H rows per lane and step: a wave step covers 4 H rows (H = 2: a whole 8-row group; H = 1 at
+    // NQ = 8, at NQ = 4 with KM = 32 and at d > 2048: half a group, which keeps the queries'
+    // dots, the lists and the prefetched codes within the register file — a spill's reload waits
+    // for every outstanding load, the prefetch too)
+    constexpr int H = (NQ * KM > 64 || NBI > 2) ? 1 : 2;
+    constexpr int kSub = 2 / H;                                  // wave steps per 8-row group
+    const int cnt = kSub * (split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0);
     // One 8-row group per wave step; two register sets, so the next group's loads are in flight
     // while this one's products run (a single set left each wave idle for a whole HBM round trip
     // per group: 4.7 TB/s with three waves per SIMD).
     struct Grp {
-        uint4 cw[2][NBI][4];     // 2 rows x NBI blocks x 64 codes
-        float sc[2][NBI];
-        float xn[2];
-        int row[2];
+        uint4 cw[H][NBI][4];     // H rows x NBI blocks x 64 codes
+        float sc[H][NBI];
+        float xn[H];
+        int row[H];
     };
     auto load = [&](int li, Grp& G) __attribute__((always_inline)) {
-        const int m = split + li * nsplit;
+        const int m = split + (li / kSub) * nsplit, r0 = m * kGroup + 4 * (li % kSub);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            G.row[h] = m * kGroup + 4 * h + g;
+        for (int h = 0; h < H; ++h) {
+            G.row[h] = r0 + 4 * h + g;
             const int rc = min(G.row[h], nrows - 1);
 #pragma unroll
             for (int bi = 0; bi < NBI; ++bi) {
@@ -261,9 +274,9 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         }
     };
     auto process = [&](Grp& G) __attribute__((always_inline)) {
-        float acc[2][NQ];
+        float acc[H][NQ];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < H; ++h)
 #pragma unroll
             for (int q = 0; q < NQ; ++q) acc[h][q] = 0.f;
 #pragma unroll
@@ -271,51 +284,58 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
             const int b = j + 16 * bi;
             // exact int32 dots of the row's 64 codes with the query block's hi and lo codes
             // (|sum| <= 64 * 127^2 < 2^24: exact in fp32 too), folded once per block:
-            // acc += s_x (s_hi D_hi + s_lo D_lo)
-            int dh[2][NQ], dl[2][NQ];
+            // acc += s_x (s_hi D_hi + s_lo D_lo); queries four at a time (NQ = 8: the dots of
+            // four queries live at once, not eight)
+            constexpr int QN = NQ < 4 ? NQ : 4;
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int q0 = 0; q0 < NQ; q0 += QN) {
+                int dh[H][QN], dl[H][QN];
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) dh[h][q] = dl[h][q] = 0;
+                for (int h = 0; h < H; ++h)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                // chunk by chunk: the laundered offset keeps this chunk's query reads below the
-                // previous chunk's (pinned) dots, so one chunk's query codes are live at a time
-                int qoff = 16 * c;
-                asm volatile("" : "+v"(qoff));
+                    for (int t = 0; t < QN; ++t) dh[h][t] = dl[h][t] = 0;
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    const uint4 hi = *reinterpret_cast<const uint4*>(&sqc[q][b][qoff]);
-                    const uint4 lo = *reinterpret_cast<const uint4*>(&sqc[q][b][kBlk + qoff]);
+                for (int c = 0; c < 4; ++c) {
+                    // chunk by chunk: the laundered offset keeps this chunk's query reads below
+                    // the previous chunk's (pinned) dots, so one chunk's query codes are live at
+                    // a time
+                    int qoff = 16 * c;
+                    asm volatile("" : "+v"(qoff));
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint4 w = G.cw[h][bi][c];
-                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.x, (int)hi.x, dh[h][q], false);
-                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.y, (int)hi.y, dh[h][q], false);
-                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.z, (int)hi.z, dh[h][q], false);
-                        dh[h][q] = __builtin_amdgcn_sdot4((int)w.w, (int)hi.w, dh[h][q], false);
-                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.x, (int)lo.x, dl[h][q], false);
-                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.y, (int)lo.y, dl[h][q], false);
-                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.z, (int)lo.z, dl[h][q], false);
-                        dl[h][q] = __builtin_amdgcn_sdot4((int)w.w, (int)lo.w, dl[h][q], false);
+                    for (int t = 0; t < QN; ++t) {
+                        const uint4 hi = *reinterpret_cast<const uint4*>(&sqc[q0 + t][b][qoff]);
+                        const uint4 lo = *reinterpret_cast<const uint4*>(&sqc[q0 + t][b][kBlk + qoff]);
+#pragma unroll
+                        for (int h = 0; h < H; ++h) {
+                            const uint4 w = G.cw[h][bi][c];
+                            dh[h][t] = __builtin_amdgcn_sdot4((int)w.x, (int)hi.x, dh[h][t], false);
+                            dh[h][t] = __builtin_amdgcn_sdot4((int)w.y, (int)hi.y, dh[h][t], false);
+                            dh[h][t] = __builtin_amdgcn_sdot4((int)w.z, (int)hi.z, dh[h][t], false);
+                            dh[h][t] = __builtin_amdgcn_sdot4((int)w.w, (int)hi.w, dh[h][t], false);
+                            dl[h][t] = __builtin_amdgcn_sdot4((int)w.x, (int)lo.x, dl[h][t], false);
+                            dl[h][t] = __builtin_amdgcn_sdot4((int)w.y, (int)lo.y, dl[h][t], false);
+                            dl[h][t] = __builtin_amdgcn_sdot4((int)w.z, (int)lo.z, dl[h][t], false);
+                            dl[h][t] = __builtin_amdgcn_sdot4((int)w.w, (int)lo.w, dl[h][t], false);
+                        }
                     }
+#pragma unroll
+                    for (int h = 0; h < H; ++h)
+#pragma unroll
+                        for (int t = 0; t < QN; ++t) asm volatile("" : "+v"(dh[h][t]), "+v"(dl[h][t]));
                 }
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
+                for (int t = 0; t < QN; ++t) {
+                    const float sh = sqs[q0 + t][b][0], sl = sqs[q0 + t][b][1];
 #pragma unroll
-                    for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(dh[h][q]), "+v"(dl[h][q]));
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const float sh = sqs[q][b][0], sl = sqs[q][b][1];
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    acc[h][q] = fmaf(G.sc[h][bi], fmaf(sl, (float)dl[h][q], sh * (float)dh[h][q]), acc[h][q]);
+                    for (int h = 0; h < H; ++h)
+                        acc[h][q0 + t] = fmaf(G.sc[h][bi], fmaf(sl, (float)dl[h][t], sh * (float)dh[h][t]),
+                                              acc[h][q0 + t]);
+                }
             }
         }
         // keys; lane j (< NQ) of the row's group inserts query j's key (rows increase per lane)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             float kv = INFINITY;
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -341,6 +361,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     }
 
     // fold the split's 16 lists of each query (4 waves x 4 row groups) into one list of KM
+    __syncthreads();                                     // (every wave is done with the codes)
     if (owner) {
 #pragma unroll
         for (int p = 0; p < KM; ++p) {

@@ -352,9 +352,9 @@ bool use_b16(const knn_index* ix, int64_t nq, int k) {
 }
 
 // AUTO: batches of <= kI8AutoQ queries on an index the bf16 path would serve as small (the int8
-// copy streams about half of the bf16 copy's bytes; the scan's LDS query reads grow with the
-// batch: nq <= 4 stays HBM-bound, nq = 5-8 is LDS-bound and slower than the bf16 pass)
-constexpr int kI8AutoQ = 4;
+// copy streams about half of the bf16 copy's bytes; its dot products grow with the batch: nq <= 4
+// is HBM-bound, nq = 5-8 VALU-bound and still faster than the bf16 pass)
+constexpr int kI8AutoQ = 8;
 bool use_i8(const knn_index* ix, int64_t nq, int k) {
     if (ix->nblk8 <= 0 || k > KNN_MAX_K || nq > kI8MaxQ) return false;
     if (ix->mode == KNN_SEARCH_I8) return true;

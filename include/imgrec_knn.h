@@ -90,7 +90,7 @@ enum knn_error {
  *       queries on an index of >= 16384 rows and for smaller batches on an index of >= 131072
  *       rows (the bf16 copy streams half the bytes); the split path when bf16 is unavailable and
  *       the batch is large; everything else the exact fp32 kernel.
- *       Batches of <= 4 queries (the reference CLI's one-query searches) on such an index take
+ *       Batches of <= 8 queries (the reference CLI's one-query searches) on such an index take
  *       the int8 path instead: a block-scaled int8 copy of the rows (one fp32 scale per 64
  *       elements, about half the bf16 copy's bytes, built on the first such search), a
  *       two-level int8 query and exact int32 dot4 products, K' = 64, the same certificate with

@@ -1,5 +1,5 @@
 """Parity tests of the int8 small-batch candidate path (include/imgrec_knn.h KNN_SEARCH_I8, the AUTO
-default for batches of <= 4 queries on an index of >= 131072 rows; csrc/knn_i8.hip).
+default for batches of <= 8 queries on an index of >= 131072 rows; csrc/knn_i8.hip).
 
 The int8 path scores rows on a block-scaled int8 copy (one fp32 scale per 64 elements) with a
 two-level int8 query (exact int32 dot4 products), reranks K' = 64 candidates in exact fp32 and certifies per query, from the stored
@@ -99,15 +99,15 @@ def test_i8_concat_layout_self_query(faiss):
 
 
 def test_i8_auto_picks_int8_for_single_queries(faiss):
-    """AUTO: one to four queries on >= 131072 rows take the int8 path, five take the bf16 path."""
+    """AUTO: one to eight queries on >= 131072 rows take the int8 path, nine take the bf16 path."""
     d = 256
     xb = mixture(140000, d, centres=200, seed=3)
-    xq = mixture(5, d, centres=200, seed=4)
+    xq = mixture(9, d, centres=200, seed=4)
     idx = faiss.IndexFlatL2(d)
     idx.add(xb)
     from oracle.flat_knn import search_exact
     orc = search_exact(xb, xq, 11, "l2")
-    for nq, path in ((1, 3), (2, 3), (3, 3), (4, 3), (5, 2)):
+    for nq, path in ((1, 3), (2, 3), (4, 3), (5, 3), (8, 3), (9, 2)):
         D, I = idx.search(xq[:nq], 10)
         assert _lib().knn_last_path(idx.handle) == path
         check_knn(D, I, xb, xq[:nq], 10, "l2", min_exact_frac=0.5,
@@ -175,7 +175,7 @@ def test_i8_clustered_storage(faiss):
 @pytest.mark.parametrize("nq", [5, 6, 8])
 @pytest.mark.parametrize("metric", ["l2", "cosine"])
 def test_i8_batches_of_five_to_eight(faiss, nq, metric):
-    """The NQ = 8 scan instance (search_mode "i8" only): every query's 16 lists are folded."""
+    """The NQ = 8 scan instance (one row per lane and step): every query's 16 lists are folded."""
     xb = mixture(12001, 300, centres=60, seed=nq)
     xq = mixture(nq, 300, centres=60, seed=nq + 50)
     idx = _index(faiss, 300, metric)

@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-r03z}; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_i8_gpu.py tests/test_sweep_gpu.py -k "i8" -x -q -m gpu --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-for nq in ${NQS:-1 2 3 4}; do
+for nq in ${NQS:-1 2 3 4 5 8}; do
   timeout -k 10 120 python bench.py --nq $nq --mode i8 --profile-only --steps 300 --warmup 100 > $OUT/nq$nq.json 2>>$OUT/err.log || exit 2
   echo "nq $nq $(cat $OUT/nq$nq.json)"
 done
