@@ -24,11 +24,20 @@ def i8(x, B=64):
     b2 = xp.reshape(n, Dp//B, B)
     s = np.abs(b2).max(-1, keepdims=True) / 127.0; s[s == 0] = 1
     return (np.rint(b2 / s) * s).reshape(n, Dp)[:, :D]
+def seg(x, bounds=(0, 48, 176, 1968)):
+    """int8 with one scale per concat part (colour 48 | SIFT 128 | DreamSim 1792)"""
+    out = np.empty_like(x)
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        s = np.abs(x[:, a:b]).max(1, keepdims=True) / 127.0; s[s == 0] = 1
+        out[:, a:b] = np.rint(x[:, a:b] / s) * s
+    return out
 def bf16(x):
     return torch.from_numpy(x.astype(np.float32)).bfloat16().double().numpy()
-variants = {"bf16": bf16, "i8b64": i8, "mxfp8": mx}
-qv = {"bf16": bf16(xq), "i8b64": xq, "mxfp8": mx(xq), "mxfp8_qexact": xq}
-rowv = {"bf16": "bf16", "i8b64": "i8b64", "mxfp8": "mxfp8", "mxfp8_qexact": "mxfp8"}
+variants = {"bf16": bf16, "i8b64": i8, "mxfp8": mx, "i8seg": seg}
+qv = {"bf16": bf16(xq), "i8b64": xq, "mxfp8": mx(xq), "mxfp8_qexact": xq, "i8seg": seg(xq),
+      "i8seg_qexact": xq}
+rowv = {"bf16": "bf16", "i8b64": "i8b64", "mxfp8": "mxfp8", "mxfp8_qexact": "mxfp8", "i8seg": "i8seg",
+        "i8seg_qexact": "i8seg"}
 AP = {v: [] for v in qv}; RR = {v: [] for v in variants}
 for blk in bench.gen_rows(torch, cfg, cent, 0, N, 'cpu', 3):
     xb = blk.numpy().astype(np.float64)
