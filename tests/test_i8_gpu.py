@@ -196,3 +196,31 @@ def test_i8_mode_batch_above_eight_served_as_auto(faiss):
     D, I = idx.search(xq, 5)
     assert _lib().knn_last_path(idx.handle) != 3
     check_knn(D, I, xb, xq, 5, "l2", min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("d", [2100, 3000, 4096])
+@pytest.mark.parametrize("nq,k", [(1, 10), (4, 32), (8, 10), (8, 32)])
+def test_i8_wide_rows_and_list_depths(faiss, d, nq, k):
+    """Rows past 2048 elements (33-64 blocks: three and four blocks per lane, one row per lane and
+    step) up to the path's 4096, with both list depths (KM = 16 for k <= 16, KM = 32 above)."""
+    xb = mixture(4001, d, centres=40, seed=d + nq)
+    xq = mixture(nq, d, centres=40, seed=d + nq + 1)
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    idx.search_mode = "i8"
+    D, I = idx.search(xq, k)
+    assert _lib().knn_last_path(idx.handle) == 3
+    _stats(idx, nq)
+    # (at these widths the mixture's neighbours sit inside the fp32 tie window: every returned
+    # label's exact distance and every rank's distance are still checked against the oracle)
+    check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.0)
+
+
+def test_i8_mode_refused_outside_its_dimensions(faiss):
+    """d < 64 or d > 4096 has no int8 copy: the setter refuses "i8" loudly."""
+    for d in (32, 4100):
+        idx = faiss.IndexFlatL2(d)
+        idx.add(mixture(100, d, centres=5, seed=d))
+        with pytest.raises(RuntimeError):
+            idx.search_mode = "i8"
+        assert idx.search_mode == "auto"
