@@ -110,34 +110,91 @@ i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t
     if (lane == 0) resid[row] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
 }
 
-// Query side: two-level int8 codes per 64-element block, q~ = s_hi c_hi + s_lo c_lo
-// (c_hi = rint(q / s_hi), s_hi = max|q_b| / 127; c_lo the same of q - s_hi c_hi), so the scan's
-// products are exact int32 dot4s and the query's own rounding |q - q~| (about 2^-14 |q|) is
-// the certificate's dq term (q_resid).  One wave per query, lane b = block b (nblk <= 64);
-// out: codes[q][b] = 64 hi | 64 lo, scales[q][b] = (s_hi, s_lo), resid[q] (inflated for its own
-// fp32 evaluation as the rows' is).
+// The int8 path's whole query side in one pass (one wave per query row): raw row (d floats) ->
+// padded fp32 row (dp, zero tail; L2-normalised when `normalize`) and |q|^2 — the same lane
+// chunks, order and reductions as query_prep_b16_kernel (knn_refine.hip), so the rows and norms
+// are bit-identical to the bf16 path's — then, from a copy of the row in LDS, the two-level int8
+// codes per 64-element block, q~ = s_hi c_hi + s_lo c_lo (c_hi = rint(q / s_hi), s_hi =
+// max|q_b| / 127; c_lo the same of q - s_hi c_hi), so the scan's products are exact int32 dot4s
+// and the query's own rounding |q - q~| (about 2^-14 |q|, inflated for its own fp32 evaluation as
+// the rows' is) is the certificate's dq term (q_resid).  Lane b = block b (nblk <= 64); out:
+// codes[q][b] = 64 hi | 64 lo, scales[q][b] = (s_hi, s_lo), resid[q].  Rows n .. n_pad-1
+// (the exact re-run tile's padding) get zero rows and norms, no codes.  dp <= 512 IT.
+template <int IT>
 __global__ void __launch_bounds__(64)
-i8_query_kernel(const float* __restrict__ qp, int dp, int nblk, int8_t* __restrict__ codes,
-                float* __restrict__ scales, float* __restrict__ resid) {
-    const int64_t q = blockIdx.x;
+i8_query_prep_kernel(const float* __restrict__ src, int64_t n, int d, int dp, int normalize,
+                     int nblk, float* __restrict__ dst, float* __restrict__ norms,
+                     int8_t* __restrict__ codes, float* __restrict__ scales,
+                     float* __restrict__ resid) {
+    constexpr int kPitch = kBlk + 1;                     // block b at b * 65: lane b's reads
+    __shared__ float srow[64 * kPitch];                  // walk distinct banks
+    const int64_t row = blockIdx.x;
     const int lane = threadIdx.x;
-    const float* x = qp + q * dp;
+    const bool real = row < n;
+    const float* s = src + row * d;
+    float e[IT][8];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int j0 = 8 * (lane + 64 * it);
+        if (real && (d & 3) == 0 && j0 + 8 <= d) {
+            const float4 v0 = *reinterpret_cast<const float4*>(s + j0);
+            const float4 v1 = *reinterpret_cast<const float4*>(s + j0 + 4);
+            e[it][0] = v0.x; e[it][1] = v0.y; e[it][2] = v0.z; e[it][3] = v0.w;
+            e[it][4] = v1.x; e[it][5] = v1.y; e[it][6] = v1.z; e[it][7] = v1.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) e[it][t] = (real && j0 + t < d) ? s[j0 + t] : 0.f;
+        }
+    }
+    float scale = 1.f;
+    if (normalize) {
+        float acc = 0.f;
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) acc = fmaf(e[it][t], e[it][t], acc);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (acc > 0.f) scale = (float)(1.0 / (double)sqrtf(acc));
+    }
+    float nacc = 0.f;
+    float* o = dst + row * dp;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int c = lane + 64 * it;
+        if (8 * c >= dp) continue;                       // dp is a multiple of 16
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            v[t] = normalize ? e[it][t] * scale : e[it][t];
+            nacc = fmaf(v[t], v[t], nacc);
+            const int i = 8 * c + t;
+            srow[(i >> 6) * kPitch + (i & 63)] = v[t];
+        }
+        *reinterpret_cast<float4*>(o + 8 * c) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(o + 8 * c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nacc += __shfl_xor(nacc, off, 64);
+    if (lane == 0) norms[row] = nacc;
+    if (!real) return;                                   // (whole wave)
+    for (int i = dp + lane; i < nblk * kBlk; i += 64) srow[(i >> 6) * kPitch + (i & 63)] = 0.f;
+    __syncthreads();
     float rsq = 0.f, xsq = 0.f;
     if (lane < nblk) {
         float v[kBlk];
         float mx = 0.f;
 #pragma unroll
-        for (int e = 0; e < kBlk; ++e) {
-            const int i = lane * kBlk + e;
-            v[e] = i < dp ? x[i] : 0.f;
-            mx = fmaxf(mx, fabsf(v[e]));
-            xsq = fmaf(v[e], v[e], xsq);
+        for (int t = 0; t < kBlk; ++t) {
+            v[t] = srow[lane * kPitch + t];
+            mx = fmaxf(mx, fabsf(v[t]));
+            xsq = fmaf(v[t], v[t], xsq);
         }
         uint32_t w[2][kBlk / 4];
         float sc[2];
 #pragma unroll
         for (int lev = 0; lev < 2; ++lev) {
-            const float s = mx / 127.f, inv = mx > 0.f ? 127.f / mx : 0.f;
+            const float sl = mx / 127.f, inv = mx > 0.f ? 127.f / mx : 0.f;
             float mx2 = 0.f;
 #pragma unroll
             for (int e4 = 0; e4 < kBlk / 4; ++e4) {
@@ -145,28 +202,28 @@ i8_query_kernel(const float* __restrict__ qp, int dp, int nblk, int8_t* __restri
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const int c = max(-127, min(127, (int)rintf(v[4 * e4 + t] * inv)));
-                    v[4 * e4 + t] -= (float)c * s;                 // the residual, next level's input
+                    v[4 * e4 + t] -= (float)c * sl;              // the residual, next level's input
                     mx2 = fmaxf(mx2, fabsf(v[4 * e4 + t]));
                     word |= ((uint32_t)c & 0xffu) << (8 * t);
                 }
                 w[lev][e4] = word;
             }
-            sc[lev] = s;
+            sc[lev] = sl;
             mx = mx2;
         }
 #pragma unroll
-        for (int e = 0; e < kBlk; ++e) rsq = fmaf(v[e], v[e], rsq);
-        uint4* dst = reinterpret_cast<uint4*>(codes + (q * nblk + lane) * 2 * kBlk);
+        for (int t = 0; t < kBlk; ++t) rsq = fmaf(v[t], v[t], rsq);
+        uint4* out = reinterpret_cast<uint4*>(codes + (row * nblk + lane) * 2 * kBlk);
 #pragma unroll
         for (int c = 0; c < 8; ++c)
-            dst[c] = make_uint4(w[c >> 2][4 * (c & 3)], w[c >> 2][4 * (c & 3) + 1],
+            out[c] = make_uint4(w[c >> 2][4 * (c & 3)], w[c >> 2][4 * (c & 3) + 1],
                                 w[c >> 2][4 * (c & 3) + 2], w[c >> 2][4 * (c & 3) + 3]);
-        scales[(q * nblk + lane) * 2] = sc[0];
-        scales[(q * nblk + lane) * 2 + 1] = sc[1];
+        scales[(row * nblk + lane) * 2] = sc[0];
+        scales[(row * nblk + lane) * 2 + 1] = sc[1];
     }
     rsq = wave_sum(rsq);
     xsq = wave_sum(xsq);
-    if (lane == 0) resid[q] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
+    if (lane == 0) resid[row] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
 }
 
 // Ascending list, labels arriving in increasing order: slot p's key is the median of (kd[p-1], d,
@@ -408,12 +465,20 @@ hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* 
     return hipGetLastError();
 }
 
-hipError_t launch_i8_query(const float* qp, int64_t nq, int dp, int nblk, int8_t* codes, float* scales,
-                           float* resid, hipStream_t st) {
-    if (nq <= 0) return hipSuccess;
-    if (nblk <= 0 || nblk > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(i8_query_kernel, dim3((unsigned)nq), dim3(64), 0, st, qp, dp, nblk, codes,
-                       scales, resid);
+hipError_t launch_i8_query_prep(const float* src, int64_t n, int d, int dp, int64_t n_pad,
+                                int normalize, int nblk, float* dst, float* norms, int8_t* codes,
+                                float* scales, float* resid, hipStream_t st) {
+    if (n_pad <= 0) return hipSuccess;
+    if (nblk <= 0 || nblk > 64 || dp % 16 != 0 || dp < d || dp > nblk * kBlk || n_pad < n)
+        return hipErrorInvalidValue;
+    const dim3 grid((unsigned)n_pad), block(64);
+#define IMGREC_I8QP(ITV) hipLaunchKernelGGL((i8_query_prep_kernel<ITV>), grid, block, 0, st, src, n, d, \
+                                            dp, normalize, nblk, dst, norms, codes, scales, resid)
+    if (dp <= 512) IMGREC_I8QP(1);
+    else if (dp <= 1024) IMGREC_I8QP(2);
+    else if (dp <= 2048) IMGREC_I8QP(4);
+    else IMGREC_I8QP(8);
+#undef IMGREC_I8QP
     return hipGetLastError();
 }
 

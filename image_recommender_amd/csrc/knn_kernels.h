@@ -188,9 +188,10 @@ __host__ __device__ inline int64_t i8_row_bytes(int nblk) { return (int64_t)1024
 hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* codes, float* scales,
                           float* resid, hipStream_t st);
 hipError_t launch_i8_scan(const I8Args& a, hipStream_t st);
-// fp32 queries (stride dp) -> two-level int8 block codes + scales + |q - q~| per query
-hipError_t launch_i8_query(const float* qp, int64_t nq, int dp, int nblk, int8_t* codes, float* scales,
-                           float* resid, hipStream_t st);
+// launch_query_prep_b16's fp32 rows and norms + the int8 query codes in one pass (knn_i8.hip)
+hipError_t launch_i8_query_prep(const float* src, int64_t n, int d, int dp, int64_t n_pad,
+                                int normalize, int nblk, float* dst, float* norms, int8_t* codes,
+                                float* scales, float* resid, hipStream_t st);
 
 hipError_t launch_rows_ingest(const float* src, int64_t n, int d, int dp, int64_t n_pad,
                               int normalize, float* dst, float* norms, hipStream_t st);

@@ -259,10 +259,7 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
     if ((rc = grow_stats(ix, nq, st)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->q8, &ix->q8_cap, (size_t)nq * ix->nblk8 * 128)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->q8s, &ix->q8s_cap, (size_t)nq * ix->nblk8 * 2)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->q8r, &ix->q8r_cap, (size_t)nq)) != KNN_OK) return rc;
-    KNN_HIP(launch_i8_query(qpad, nq, ix->dp, ix->nblk8, ix->q8, ix->q8s, ix->q8r, st));
+    // (the query's int8 codes ix->q8 / q8s / q8r come with qpad from launch_i8_query_prep)
     I8Args a{};
     a.codes = ix->x8; a.scales = ix->x8s; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
     a.nblk = ix->nblk8; a.qcodes = ix->q8; a.qscales = ix->q8s; a.qnorm = qnorm; a.nq = (int)nq;
@@ -401,9 +398,17 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nq_pad * ix->dp)) != KNN_OK) return rc;
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nq_pad)) != KNN_OK) return rc;
         bool q_ready = false;
-        // fused query prep: fp32 padded rows + norms + bf16 + residuals (the int8 path uses its
-        // fp32 rows and norms: one short pass instead of rows_ingest's latency-bound row loop)
-        if ((b16 || i8) && ix->dpb <= 4096) {
+        // fused query prep: fp32 padded rows + norms + bf16 + residuals, or for the int8 path
+        // the same rows and norms + the two-level int8 codes (one short pass instead of
+        // rows_ingest's latency-bound row loop and a second launch)
+        if (i8) {
+            if ((rc = grow(&ix->q8, &ix->q8_cap, (size_t)cn * ix->nblk8 * 128)) != KNN_OK) return rc;
+            if ((rc = grow(&ix->q8s, &ix->q8s_cap, (size_t)cn * ix->nblk8 * 2)) != KNN_OK) return rc;
+            if ((rc = grow(&ix->q8r, &ix->q8r_cap, (size_t)cn)) != KNN_OK) return rc;
+            KNN_HIP(launch_i8_query_prep(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
+                                         ix->nblk8, ix->qpad, ix->qnorm, ix->q8, ix->q8s, ix->q8r, st));
+            q_ready = true;
+        } else if (b16 && ix->dpb <= 4096) {
             if ((rc = grow(&ix->qb16, &ix->qb16_cap, (size_t)nq_pad * ix->dpb)) != KNN_OK) return rc;
             if ((rc = grow(&ix->q_resid, &ix->q_resid_cap, (size_t)nq_pad)) != KNN_OK) return rc;
             KNN_HIP(launch_query_prep_b16(q + c0 * ix->d, cn, ix->d, ix->dp, ix->dpb, nq_pad,
