@@ -24,6 +24,7 @@
 
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <stdint.h>
 #include <float.h>
@@ -1051,8 +1052,10 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
 // the highest bit where the smallest and largest valid value differ — and the row bits only when
 // the K-th key is tied.  The K winners are compacted by a block scan and each placed at its rank.
 // Floor = min(floor_in of every list, when given; the last key of every full list).
-// Used as the second level after cand_merge_lane_kernel (NT 256, G <= 64 lists of <= 64), where
-// it replaced a one-wave LDS-queue merge (32.5 -> 17.3 us per query at nq = 1).  Measured and
+// The second level after cand_merge_lane_kernel (NT 256, G <= 64 lists of <= 64) when level 1
+// keeps kout per group (kout <= 16, or IMGREC_MERGE_K1=0), where it replaced a one-wave LDS-queue
+// merge (32.5 -> 17.3 us per query at nq = 1); with 16 per group the second level is one more
+// lane-kernel wave (16.0 -> ~7 us at nq = 1, round 3).  Measured and
 // dropped: the whole merge of a small batch in one 1024-thread block per query (2048 lists x 16
 // at nq = 1, 32 entries per thread): 50.1 us against the two levels' 32 us — one CU's VALU
 // issue of the counts, where level 1 spreads the lists over 32 waves on as many CUs
@@ -1193,9 +1196,28 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
             else IMGREC_CAND_LANE(16, nq, nlists, 1, stride_q, stride_l, kout, nullptr, 0, D, I, floor);
             return hipGetLastError();
         }
-        // level 1: each group of 64 lists -> its kout best (+ floor: a group that keeps fewer
-        // than kout would cap the certificate at that group's last key); level 2: the G lists
+        // level 1: each group of 64 lists -> its k1 best (+ floor: a group that keeps fewer
+        // than kout would cap the certificate at that group's last key); level 2: the G lists.
+        // k1 = 16 when kout > 16: a group rarely holds more than 16 of the kout best (at G = 12,
+        // ~5), and when it does its full list's 16th key is the floor the certificate then
+        // uses; level 2 is then one more wave (G lists of 16) instead of a block select over
+        // G x kout.  IMGREC_MERGE_K1=0 keeps k1 = kout.
+        static const bool k1_16 = [] {
+            const char* e = std::getenv("IMGREC_MERGE_K1");
+            return !(e && *e == '0');
+        }();
         const int64_t nsub = nq * (int64_t)G;
+        if (k1_16 && kout > 16) {
+            if (kin == 8) IMGREC_CAND_LANE(8, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+            else if (kin == 10) IMGREC_CAND_LANE(10, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+            else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
+            hipError_t e1 = hipGetLastError();
+            if (e1 != hipSuccess) return e1;
+            cd_ = ws_d;
+            ci_ = ws_i;
+            IMGREC_CAND_LANE(16, nq, G, 1, (int64_t)G * 16, 16, kout, ws_floor, G, D, I, floor);
+            return hipGetLastError();
+        }
         if (kin == 8) IMGREC_CAND_LANE(8, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
         else if (kin == 10) IMGREC_CAND_LANE(10, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
         else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, kout, nullptr, 0, ws_d, ws_i, ws_floor);
