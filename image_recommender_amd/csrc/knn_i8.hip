@@ -39,6 +39,10 @@ namespace {
 constexpr int kBlk = 64;       // elements per scale block
 constexpr int kWaves = 4;
 constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA piece)
+#ifndef IMGREC_I8_NT
+#define IMGREC_I8_NT 1
+#endif
+constexpr bool kNtCodes = IMGREC_I8_NT != 0;   // non-temporal code loads in the scan
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -324,7 +328,15 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
                 // contiguous bytes per load (slots of blocks >= nblk hold zeros)
                 const uint4* src = reinterpret_cast<const uint4*>(codes + (int64_t)rc * rowb) + 64 * bi + j;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) G.cw[h][bi][c] = src[16 * c];
+                for (int c = 0; c < 4; ++c) {
+                    if constexpr (kNtCodes) {    // streamed once per search: non-temporal loads
+                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 16 * c));
+                        G.cw[h][bi][c] = make_uint4(w.x, w.y, w.z, w.w);
+                    } else {
+                        G.cw[h][bi][c] = src[16 * c];
+                    }
+                }
                 G.sc[h][bi] = b < nblk ? scales[(int64_t)rc * nblk + b] : 0.f;
             }
             G.xn[h] = l2 ? xnorm[rc] : 0.f;
