@@ -336,27 +336,28 @@ int split_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq
 
 }  // namespace
 
-// AUTO: large batches are matrix-bound (bf16 MFMA vs fp32 MFMA) once the corpus amortises the
-// rerank; small batches are HBM-bound (the bf16 copy streams half the bytes) once the corpus is
-// large enough to repay the candidate path's fixed cost (~0.1-0.2 ms).
-constexpr int64_t kB16MinRowsLarge = 16384, kB16MinRowsSmall = 131072;
+// AUTO: the bf16 path at every corpus size.  Large batches are matrix-bound (bf16 MFMA vs fp32
+// MFMA), small ones HBM-bound (the bf16 copy streams half the bytes), and on small corpora the
+// exact kernel has a latency floor of its own: one 256-row tile's whole depth of fp32 MFMAs per
+// workgroup, ~0.16 ms from 1000 rows up, against the candidate path's ~0.05-0.1 ms
+// (profiles/r03/small_corpora/: 1000-131072 rows x nq 9-1024, bf16 1.8-2.8x faster).
 bool use_b16(const knn_index* ix, int64_t nq, int k) {
     if (!ix->b16_ok || k > KNN_MAX_K) return false;
     if (ix->mode == KNN_SEARCH_BF16) return true;
     // (I8 mode: batches the int8 path does not take are served as AUTO serves them)
-    if (ix->mode != KNN_SEARCH_AUTO && ix->mode != KNN_SEARCH_I8) return false;
-    return ix->ntotal >= (nq > 128 ? kB16MinRowsLarge : kB16MinRowsSmall);
+    return ix->mode == KNN_SEARCH_AUTO || ix->mode == KNN_SEARCH_I8;
 }
 
-// AUTO: batches of <= kI8AutoQ queries on an index the bf16 path would serve as small (the int8
-// copy streams about half of the bf16 copy's bytes; its dot products grow with the batch: nq <= 4
-// is HBM-bound, nq = 5-8 VALU-bound and still faster than the bf16 pass)
+// AUTO: batches of <= kI8AutoQ queries at every corpus size (the int8 copy streams about half of
+// the bf16 copy's bytes; its dot products grow with the batch: nq <= 4 is HBM-bound, nq = 5-8
+// VALU-bound and still faster than the bf16 pass; one query on 1000-65536 rows 0.05-0.075 ms
+// against the exact kernel's 0.18-0.22, profiles/r03/small_corpora/)
 constexpr int kI8AutoQ = 8;
 bool use_i8(const knn_index* ix, int64_t nq, int k) {
     if (ix->nblk8 <= 0 || k > KNN_MAX_K || nq > kI8MaxQ) return false;
     if (ix->mode == KNN_SEARCH_I8) return true;
     if (ix->mode != KNN_SEARCH_AUTO) return false;
-    return nq <= kI8AutoQ && ix->ntotal >= kB16MinRowsSmall;
+    return nq <= kI8AutoQ;
 }
 
 bool use_split(const knn_index* ix, int64_t nq, int k) {

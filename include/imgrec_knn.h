@@ -86,12 +86,13 @@ enum knn_error {
  * data), but only the rigorous window is a promise.  A query whose certificate fails gets a second chance (every
  * per-split list entry reranked, certified against the list floor); if that fails too it is
  * re-run on the exact fp32 kernel, planned on the device.
- * AUTO: the bf16 path (d >= 64; one bf16 MFMA per product, K' = 64) for batches of > 128
- *       queries on an index of >= 16384 rows and for smaller batches on an index of >= 131072
- *       rows (the bf16 copy streams half the bytes); the split path when bf16 is unavailable and
- *       the batch is large; everything else the exact fp32 kernel.
- *       Batches of <= 8 queries (the reference CLI's one-query searches) on such an index take
- *       the int8 path instead: a block-scaled int8 copy of the rows (one fp32 scale per 64
+ * AUTO: the bf16 path (d >= 64; one bf16 MFMA per product, K' = 64) for every batch at every
+ *       corpus size (large batches: bf16 MFMA; small ones: the bf16 copy streams half the
+ *       bytes; small corpora: the exact kernel's latency floor of ~0.16 ms per search); the
+ *       split path when bf16 is unavailable and the batch is large; everything else (d < 64,
+ *       k > KNN_MAX_K) the exact fp32 kernel.
+ *       Batches of <= 8 queries (the reference CLI's one-query searches) take the int8 path
+ *       instead (64 <= d <= 4096): a block-scaled int8 copy of the rows (one fp32 scale per 64
  *       elements, about half the bf16 copy's bytes, built on the first such search), a
  *       two-level int8 query and exact int32 dot4 products, K' = 64, the same certificate with
  *       the int8 copy's and the query's residual bounds (csrc/knn_i8.hip).

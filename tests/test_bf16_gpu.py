@@ -245,9 +245,9 @@ def test_bf16_big_tile_self_query_concat(faiss):
 
 @pytest.mark.parametrize("nq", [1, 5, 64])
 def test_auto_small_batch_on_large_corpus_takes_bf16(faiss, nq):
-    """AUTO routes small batches on corpora of >= 131072 rows to the bf16 path (HBM-bound: the
-    bf16 copy streams half the bytes); many row splits per query exercise the two-level
-    candidate merge."""
+    """AUTO routes small batches to a candidate path (int8 for <= 8 queries, bf16 above: the
+    copies stream a quarter / half of the fp32 bytes); many row splits per query exercise the
+    two-level candidate merge."""
     xb = mixture(140000, 256, centres=300, seed=41)
     xq = mixture(nq, 256, centres=300, seed=42)
     idx = faiss.IndexFlatL2(256)

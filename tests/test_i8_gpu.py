@@ -1,5 +1,5 @@
 """Parity tests of the int8 small-batch candidate path (include/imgrec_knn.h KNN_SEARCH_I8, the AUTO
-default for batches of <= 8 queries on an index of >= 131072 rows; csrc/knn_i8.hip).
+default for batches of <= 8 queries; csrc/knn_i8.hip).
 
 The int8 path scores rows on a block-scaled int8 copy (one fp32 scale per 64 elements) with a
 two-level int8 query (exact int32 dot4 products), reranks K' = 64 candidates in exact fp32 and certifies per query, from the stored
@@ -99,7 +99,7 @@ def test_i8_concat_layout_self_query(faiss):
 
 
 def test_i8_auto_picks_int8_for_single_queries(faiss):
-    """AUTO: one to eight queries on >= 131072 rows take the int8 path, nine take the bf16 path."""
+    """AUTO: one to eight queries take the int8 path, nine the bf16 path."""
     d = 256
     xb = mixture(140000, d, centres=200, seed=3)
     xq = mixture(9, d, centres=200, seed=4)

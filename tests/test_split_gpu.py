@@ -166,18 +166,27 @@ def test_split_tiny_corpus_and_id_offset(faiss):
 
 
 def test_auto_mode_routing(faiss):
-    """AUTO: large batches take a candidate path (bf16 when available), small ones the exact
-    kernel."""
+    """AUTO: every batch on a candidate path at every corpus size (bf16; int8 for <= 8 queries);
+    the exact kernel only for d < 64, k past the fused lists and search_mode "exact"."""
+    from image_recommender_amd import _lib
     xb = mixture(20000, 512, centres=100, seed=31)
     idx = faiss.IndexFlatL2(512)
     idx.add(xb)
     assert idx.search_mode == "auto"
     xq = mixture(300, 512, centres=100, seed=32)
-    D, I = idx.search(xq, 10)
-    assert idx.search_stats()[0] == 300
-    check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5)
+    for nq, path in ((300, 2), (64, 2), (9, 2), (8, 3), (1, 3)):
+        D, I = idx.search(xq[:nq], 10)
+        assert _lib.load().knn_last_path(idx.handle) == path, nq
+        assert idx.search_stats()[0] == nq
+        check_knn(D, I, xb, xq[:nq], 10, "l2", min_exact_frac=0.5)
+    idx.search_mode = "exact"
     idx.search(xq[:64], 10)
-    assert idx.search_stats() == (0, 0)                   # small batch: exact kernel
+    assert _lib.load().knn_last_path(idx.handle) == 0
+    assert idx.search_stats() == (0, 0)
+    small = faiss.IndexFlatL2(48)                         # d < 64: no bf16 / int8 copy
+    small.add(mixture(3000, 48, centres=20, seed=33))
+    small.search(mixture(4, 48, centres=20, seed=34), 10)
+    assert _lib.load().knn_last_path(small.handle) == 0
 
 
 def test_split_mode_rejected_for_small_d(faiss):
