@@ -92,7 +92,8 @@ enum knn_error {
  *       split path when bf16 is unavailable and the batch is large; everything else (d < 64,
  *       k > KNN_MAX_K) the exact fp32 kernel.
  *       Batches of <= 8 queries (the reference CLI's one-query searches) take the int8 path
- *       instead (64 <= d <= 4096): a block-scaled int8 copy of the rows (one fp32 scale per 64
+ *       instead (64 <= d <= 4096; at d <= 512, where an int8 row's 1-KiB group is wider than
+ *       its bf16 row, only while the int8 copy is <= 64 MB): a block-scaled int8 copy of the rows (one fp32 scale per 64
  *       elements, about half the bf16 copy's bytes, built on the first such search), a
  *       two-level int8 query and exact int32 dot4 products, K' = 64, the same certificate with
  *       the int8 copy's and the query's residual bounds (csrc/knn_i8.hip).
