@@ -163,7 +163,11 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s, nq=1024):
     searches, against all N rows, until about budget_s of CPU work (at least one batch).
     """
     from oracle.flat_knn import search_blas_fp32_blocked
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    try:
+        allowed = len(os.sched_getaffinity(0))       # the cores this process may run on
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or allowed
     try:
         from threadpoolctl import threadpool_info
         blas = max([p.get("num_threads", 1) for p in threadpool_info()
@@ -191,6 +195,7 @@ def cpu_baseline(torch, cfg, centres, D, k, seed, budget_s, nq=1024):
     return {
         "value": nq / t, "unit": "queries/s", "cores": int(max(blas, threads)), "kind": "port",
         "cpu_model": cpu_model(), "blas_threads": int(blas), "topk_threads": int(threads),
+        "affinity_cores": int(allowed), "host_cpus": int(os.cpu_count() or 0),
         "sample": (f"all {n} rows x {d} of the workload's corpus, {nq} queries per batch (the GPU "
                    f"step's batch), median of {len(times)} batches of {t:.2f} s; "
                    f"oracle.flat_knn.search_blas_fp32_blocked = faiss IndexFlatL2 "
@@ -311,6 +316,10 @@ def main():
     build_s = time.perf_counter() - t_build0
     lib = _lib.load()
     shard.index.search_mode = a.mode
+    # every search of this process runs on torch's current stream, which lives as long as the
+    # process: the lazy fence is safe here and saves one event record (~6 us of GPU time) per step
+    # (include/imgrec_knn.h knn_set_fence_mode)
+    shard.index.set_fence_mode(lazy=True)
 
     def step():
         return shard.search(q, a.k)
@@ -349,6 +358,38 @@ def main():
             dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return float(v[0]), (float(v[1]) if kernel_events else None), out
 
+    def phases(steps):
+        """Per-rank phase times of `steps` searches (a diagnostic region after the timed ones:
+        its event records cost GPU time): this rank's local search (query prep, candidate kernel,
+        merge, rerank, certificate tail), the all-gather of the packed chunks, the final merge, and
+        the candidate kernel alone; plus where this rank runs.  Gathered to every rank."""
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        lib.knn_set_timing(h, 1)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        for e in evs:
+            shard.search(q, a.k, events=e)
+        torch.cuda.synchronize()
+        tot_ms, nl = C.c_double(), C.c_int()
+        _lib.check(lib.knn_kernel_time(h, C.byref(tot_ms), C.byref(nl)), "timing")
+        lib.knn_set_timing(h, 0)
+        t = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])]
+                      for e in evs])
+        props = torch.cuda.get_device_properties(device)
+        rec = {"rank": rank, "device": f"cuda:{local}",
+               "pci_bus_id": (f"{getattr(props, 'pci_domain_id', 0):04x}:{getattr(props, 'pci_bus_id', 0):02x}:"
+                              f"{getattr(props, 'pci_device_id', 0):02x}"),
+               "rows": shard.local_rows, "local_search_ms": float(np.median(t[:, 0])),
+               "candidate_kernel_ms": tot_ms.value / max(nl.value, 1),
+               "allgather_ms": float(np.median(t[:, 1])), "merge_ms": float(np.median(t[:, 2])),
+               "steps": steps}
+        if world > 1:
+            allrec = [None] * world
+            dist.all_gather_object(allrec, rec)
+            return allrec
+        return [rec]
+
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -356,12 +397,14 @@ def main():
     split_q, fallback_q, err_ratio = shard.index.search_stats(with_error=True)   # last step
     path = lib.knn_last_path(h)                                # 0 exact, 1 split, 2 bf16, 3 i8
     kel, kern_ms, _ = region(step, a.steps, True)               # candidate-kernel duration
+    per_rank = phases(a.steps)
     if a.profile_only:
         if rank == 0:
             print(json.dumps({"elapsed_s": elapsed, "ms_per_step": elapsed / a.steps * 1e3,
                               "ms_per_step_with_kernel_events": kel / a.steps * 1e3,
                               "kernel_ms": kern_ms, "split_queries": split_q,
-                              "fallback_queries": fallback_q, "err_ratio": err_ratio}))
+                              "fallback_queries": fallback_q, "err_ratio": err_ratio,
+                              "world_size": world, "per_rank": per_rank}))
         if world > 1:
             dist.destroy_process_group()
         return
@@ -477,6 +520,8 @@ def main():
                 "fp32_equivalent_gbs": bytes1 / (kern1_ms * 1e-3) / 1e9,
             },
             "build_s": build_s,
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "per_rank": per_rank,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

@@ -19,6 +19,7 @@ KNN_METRIC_IP, KNN_METRIC_L2, KNN_METRIC_COSINE = 0, 1, 2
 KNN_MAX_K = 32          # fused top-k kernels (include/imgrec_knn.h)
 KNN_MAX_K_LARGE = 1024  # largest k of a search (GEMM + select beyond KNN_MAX_K)
 KNN_SEARCH_AUTO, KNN_SEARCH_EXACT, KNN_SEARCH_SPLIT, KNN_SEARCH_BF16, KNN_SEARCH_I8 = 0, 1, 2, 3, 4
+KNN_FENCE_EAGER, KNN_FENCE_LAZY = 0, 1
 COLOR_HIST_MAX_BINS = 32
 INGEST_NOT_FAST, INGEST_TOO_SMALL = -1, -2
 
@@ -56,6 +57,7 @@ SIGNATURES = {
     "knn_read_multi": (_i, [C.c_char_p, _pi, _i, C.POINTER(_vp)]),
     "knn_normalize_L2": (_i, [_vp, _i64, _i]),
     "knn_set_timing": (_i, [_vp, _i]),
+    "knn_set_fence_mode": (_i, [_vp, _i]),
     "knn_kernel_time": (_i, [_vp, _pd, _pi]),
     "knn_plan": (_i, [_vp, _i64, _i, _pi, _pi, _pi, _pi]),
     "knn_plan_kernel": (_i, [_vp, _i64, _i, C.c_char_p, _i]),

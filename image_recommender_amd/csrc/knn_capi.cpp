@@ -12,6 +12,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "knn_index.h"
@@ -34,25 +35,47 @@ void set_err(const char* fmt, ...) {
 
 const char* last_error() { return g_err.c_str(); }
 
-// The fence is recorded lazily: an operation only remembers its stream, and the event is
-// recorded on that stream when (and only when) a later operation arrives on a different one.  The
-// event then marks the stream's current tail, which includes every earlier operation on the index
-// (and possibly later unrelated work of the caller: a conservative, still correct wait).  A stream
-// that never changes pays nothing — an event record costs ~5.7 us of GPU time per call on MI355X
-// (the gap it leaves between the kernels around it, profiles/r03/), more than the near-empty
-// kernels of a search.  The stream of an operation must therefore stay valid until the next
-// operation on the index is enqueued (include/imgrec_knn.h, Conventions).
+// Fences.  By default (KNN_FENCE_EAGER) an asynchronous operation records the index's fence
+// event on its stream as its last enqueued step, and the next operation on ANOTHER stream waits
+// for that event: nothing depends on the old stream afterwards (it may be destroyed, and work the
+// caller queues on it later is not waited for).  KNN_FENCE_LAZY (opt-in, knn_set_fence_mode)
+// records nothing while the stream stays the same and records the event on the remembered stream
+// only when a different stream arrives: back-to-back operations on one stream then pay no event
+// record (each costs ~5.7 us of idle GPU between the kernels around it on MI355X,
+// profiles/r03/), but the remembered stream must stay valid until that next operation, and the
+// wait covers whatever the caller queued on it meanwhile.  A lazy record that fails (a destroyed
+// stream) falls back to a device-wide synchronisation instead of wedging the index.
+// Host-pointer operations synchronise their stream before returning and leave no fence.
 int fence_begin(knn_index* ix, hipStream_t st) {
-    if (ix->fence_set && ix->fence_stream != st) {
-        KNN_HIP(hipEventRecord(ix->fence, ix->fence_stream));
-        KNN_HIP(hipStreamWaitEvent(st, ix->fence, 0));
+    if (!ix->fence_set || ix->fence_stream == st) return KNN_OK;
+    if (!ix->fence_recorded) {
+        if (hipEventRecord(ix->fence, ix->fence_stream) != hipSuccess) {
+            (void)hipGetLastError();
+            ix->fence_set = false;
+            KNN_HIP(hipDeviceSynchronize());
+            return KNN_OK;
+        }
+        ix->fence_recorded = true;
     }
+    KNN_HIP(hipStreamWaitEvent(st, ix->fence, 0));
     return KNN_OK;
 }
 
 int fence_end(knn_index* ix, hipStream_t st) {
     ix->fence_stream = st;
     ix->fence_set = true;
+    ix->fence_recorded = false;
+    if (!ix->fence_lazy) {
+        KNN_HIP(hipEventRecord(ix->fence, st));
+        ix->fence_recorded = true;
+    }
+    return KNN_OK;
+}
+
+// After a host-synchronous operation (its stream drained before returning): nothing to wait for.
+int fence_end_synced(knn_index* ix) {
+    ix->fence_set = false;
+    ix->fence_recorded = false;
     return KNN_OK;
 }
 
@@ -219,6 +242,11 @@ int create_single(int d, int metric, int device, knn_index** out) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)
         ix->cus = cus;
+    // IMGREC_CUS=n (tests): plan launches for n CUs, as on a partitioned device (CPX mode)
+    if (const char* e = std::getenv("IMGREC_CUS")) {
+        const int v = std::atoi(e);
+        if (v > 0 && v < ix->cus) ix->cus = v;
+    }
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ix->fence, hipEventDisableTiming) != hipSuccess) {
         if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -359,7 +387,7 @@ int knn_add(knn_index_t* ix, const float* x, int64_t n) {
         if ((rc = add_device_locked(ix, ix->hq, cn, ix->stream)) != KNN_OK) return rc;
         KNN_HIP(hipStreamSynchronize(ix->stream));
     }
-    return fence_end(ix, ix->stream);
+    return fence_end_synced(ix);
 }
 
 int knn_reset(knn_index_t* ix) {
@@ -385,9 +413,8 @@ int knn_reconstruct_n(const knn_index_t* cix, int64_t i0, int64_t n, float* x) {
     if ((rc = fence_begin(ix, ix->stream)) != KNN_OK) return rc;
     KNN_HIP(hipMemcpy2DAsync(x, (size_t)ix->d * 4, ix->xb + (size_t)i0 * ix->dp, (size_t)ix->dp * 4,
                              (size_t)ix->d * 4, (size_t)n, hipMemcpyDeviceToHost, ix->stream));
-    if ((rc = fence_end(ix, ix->stream)) != KNN_OK) return rc;
     KNN_HIP(hipStreamSynchronize(ix->stream));
-    return KNN_OK;
+    return fence_end_synced(ix);
 }
 
 int knn_search_device(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
@@ -453,8 +480,8 @@ int knn_search(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int
                            hipMemcpyDeviceToHost, ix->stream));
     KNN_HIP(hipMemcpyAsync(pinned ? ix->pi : I, ix->hi, (size_t)nq * k * sizeof(int64_t),
                            hipMemcpyDeviceToHost, ix->stream));
-    if ((rc = fence_end(ix, ix->stream)) != KNN_OK) return rc;
     KNN_HIP(hipStreamSynchronize(ix->stream));
+    if ((rc = fence_end_synced(ix)) != KNN_OK) return rc;
     if (pinned) {
         std::memcpy(D, ix->pd, (size_t)nq * k * sizeof(float));
         std::memcpy(I, ix->pi, (size_t)nq * k * sizeof(int64_t));
@@ -516,6 +543,18 @@ int knn_set_timing(knn_index_t* ix, int enable) {
     std::lock_guard<std::mutex> lk(ix->mu);
     ix->timing = enable != 0;
     ix->ev_used = 0;
+    return KNN_OK;
+}
+
+int knn_set_fence_mode(knn_index_t* ix, int mode) {
+    if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
+    if (mode != KNN_FENCE_EAGER && mode != KNN_FENCE_LAZY) KNN_FAIL(KNN_EINVAL, "unknown fence mode %d", mode);
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (ix->multi) {
+        int rc = multi_set_fence_mode(ix, mode);
+        if (rc != KNN_OK) return rc;
+    }
+    ix->fence_lazy = mode == KNN_FENCE_LAZY;
     return KNN_OK;
 }
 

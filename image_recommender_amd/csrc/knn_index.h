@@ -116,12 +116,16 @@ struct knn_index {
     int64_t last_split_queries = 0;   // queries of the last search on a candidate path
     hipStream_t stream = nullptr;     // the index's own stream (host-pointer entry points)
     std::mutex mu;
-    // Cross-stream ordering: every operation enqueued on the index remembers its stream; an
-    // operation on a different stream first records `fence` on the remembered stream and waits
-    // for it (adds before searches, one search's workspace use before the next's, ...).
+    // Cross-stream ordering: an asynchronous operation records `fence` on its stream when it ends
+    // (KNN_FENCE_EAGER, the default) or only remembers the stream and records the event there
+    // when a later operation arrives on a different stream (KNN_FENCE_LAZY, opt-in); an operation
+    // on a different stream waits for the event (adds before searches, one search's workspace use
+    // before the next's, ...).  Host-synchronous operations leave no fence.
     hipEvent_t fence = nullptr;
     hipStream_t fence_stream = nullptr;
-    bool fence_set = false;
+    bool fence_set = false;        // an operation on fence_stream may still run
+    bool fence_recorded = false;   // `fence` already marks its end
+    bool fence_lazy = false;
     // search workspace
     float* qpad = nullptr; size_t qpad_cap = 0;
     float* qnorm = nullptr; size_t qnorm_cap = 0;
@@ -182,6 +186,7 @@ int set_metric(knn_index* ix, int metric);
 int set_trained(knn_index* ix, bool trained);
 int fence_begin(knn_index* ix, hipStream_t st);
 int fence_end(knn_index* ix, hipStream_t st);
+int fence_end_synced(knn_index* ix);
 int reserve_rows(knn_index* ix, int64_t need, hipStream_t st);
 int add_device_locked(knn_index* ix, const float* x, int64_t n, hipStream_t st);
 int ensure_split(knn_index* ix, hipStream_t st);

@@ -14,6 +14,7 @@
 // its labels, and its (nq, k) result lands in a [ndev][nq][k] gather buffer on the first device
 // (peer copy over xGMI), where knn_merge's kernel produces the final rows.  The same shard merge as
 // the torchrun path (sharded.py), with device-to-device copies instead of an RCCL all-gather.
+#include <cstdlib>
 #include <cstring>
 
 #include "knn_multi.h"
@@ -35,6 +36,9 @@ struct knn_multi {
     std::vector<size_t> sx_cap;
     std::vector<hipEvent_t> done;                // per shard (its device)
     hipEvent_t ready = nullptr;                  // inputs ready on the first device
+    // IMGREC_MULTI_FORCE_REMOTE=1 (tests): shards on the first device take the other devices'
+    // staging + peer-copy path too, so one GPU exercises it
+    bool force_remote = false;
     float* gD = nullptr; size_t gD_cap = 0;      // [ndev][nq][k] on the first device
     int64_t* gI = nullptr; size_t gI_cap = 0;
 };
@@ -104,6 +108,7 @@ int multi_create(int d, int metric, const int* devices, int ndev, knn_index** ou
     knn_multi* m = new knn_multi();
     ix->multi = m;
     m->devices.assign(devices, devices + ndev);
+    if (const char* e = std::getenv("IMGREC_MULTI_FORCE_REMOTE")) m->force_remote = std::atoi(e) != 0;
     m->lmap.assign(ndev, nullptr);
     m->lmap_cap.assign(ndev, 0);
     m->sq.assign(ndev, nullptr);
@@ -213,7 +218,7 @@ int multi_add_device(knn_index* ix, const float* x, int64_t n, hipStream_t st) {
         const int64_t r0 = piece0(n, s, ndev), r1 = piece0(n, s + 1, ndev);
         if (r1 <= r0) continue;
         const float* src = x + r0 * ix->d;
-        if (sh->device == ix->device) {
+        if (sh->device == ix->device && !m->force_remote) {
             if ((rc = knn_add_device(sh, src, r1 - r0, st)) != KNN_OK) return rc;
             continue;
         }
@@ -273,7 +278,7 @@ int fan_out_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, i
     }
     for (int s = 0; s < ndev; ++s) {
         knn_index* sh = m->shards[s];
-        const bool local = sh->device == ix->device;
+        const bool local = sh->device == ix->device && !m->force_remote;
         DeviceGuard g(sh->device);
         std::lock_guard<std::mutex> lk(sh->mu);
         const hipStream_t ss = sh->stream;
@@ -352,9 +357,8 @@ int multi_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int
                            ix->stream));
     KNN_HIP(hipMemcpyAsync(I, ix->hi, (size_t)nq * k * sizeof(int64_t), hipMemcpyDeviceToHost,
                            ix->stream));
-    if ((rc = fence_end(ix, ix->stream)) != KNN_OK) return rc;
     KNN_HIP(hipStreamSynchronize(ix->stream));
-    return KNN_OK;
+    return fence_end_synced(ix);
 }
 
 int multi_set_metric(knn_index* ix, int metric) {
@@ -390,6 +394,14 @@ int multi_kernel_time(knn_index* ix, double* total_ms, int* launches) {
     }
     *total_ms = tot;
     *launches = n;
+    return KNN_OK;
+}
+
+int multi_set_fence_mode(knn_index* ix, int mode) {
+    for (knn_index* sh : M(ix)->shards) {
+        std::lock_guard<std::mutex> lk(sh->mu);
+        sh->fence_lazy = mode == KNN_FENCE_LAZY;
+    }
     return KNN_OK;
 }
 

@@ -23,6 +23,7 @@ int multi_set_trained(knn_index* ix, bool trained);
 int multi_set_timing(knn_index* ix, int enable);
 int multi_kernel_time(knn_index* ix, double* total_ms, int* launches);
 int multi_set_search_mode(knn_index* ix, int mode);
+int multi_set_fence_mode(knn_index* ix, int mode);
 int multi_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int64_t* second_q,
                        float* ratio);
 int multi_last_path(const knn_index* ix);

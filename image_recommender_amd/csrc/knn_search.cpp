@@ -104,8 +104,11 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     const int64_t cap_rows = round_up(nq, 32);
     const int bm = 128 * kFallbackWR;
     const int lists_km = 2 * kFallbackWR * km;
-    // candidate lists: at most `grid` (query block, row split) items of 32 queries each
-    const size_t ncap = (size_t)grid * 32 * lists_km;
+    // candidate lists of the exact re-run: nqb query blocks x nsplit = max(1, grid / nqb) row
+    // splits, lists_km entries per (query, split).  nqb * nsplit <= grid while nqb <= grid; past
+    // that (more than 32 x grid uncertified queries: a device with fewer CUs) nsplit = 1 and the
+    // lists need cap_rows x lists_km (sizing by the grid alone overflowed there)
+    const size_t ncap = (size_t)std::max<int64_t>(grid, cap_rows / 32) * 32 * lists_km;
     int rc;
     if ((rc = grow(&ix->fb_q, &ix->fb_q_cap, (size_t)cap_rows * ix->dp)) != KNN_OK) return rc;
     if ((rc = grow(&ix->fb_qn, &ix->fb_qn_cap, (size_t)cap_rows)) != KNN_OK) return rc;
@@ -122,7 +125,8 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
             const int v = e ? std::atoi(e) : 0;
             return v > 0 ? v : 64;
         }();
-        r.sc_slices = std::max(1, std::min({kSlices, r.raw_lists, 1024 / k}));
+        // (<= 64: the last slice's merge reads the slice heads from the lanes of one wave)
+        r.sc_slices = std::max(1, std::min({kSlices, 64, r.raw_lists, 1024 / k}));
         const size_t ns = (size_t)nq * r.sc_slices * k;
         if ((rc = grow(&ix->sc_key, &ix->sc_key_cap, ns)) != KNN_OK) return rc;
         if ((rc = grow(&ix->sc_lab, &ix->sc_lab_cap, ns)) != KNN_OK) return rc;
@@ -455,9 +459,14 @@ int read_search_stats(knn_index* ix, int64_t* split_q, int64_t* fallback_q, int6
     int acc[4] = {0, 0, 0, 0};
     KNN_HIP(hipMemcpyAsync(acc, ix->stat + 8, sizeof(acc), hipMemcpyDeviceToHost, ix->stream));
     KNN_HIP(hipStreamSynchronize(ix->stream));
-    if (acc[3] != 0)          // cert_tail_kernel's bounded wait for its planner ran out
+    if (acc[3] != 0) {        // cert_tail_kernel's bounded wait for its planner ran out
+        // reported once: clear the bit so later clean searches read their stats again
+        const int zero = 0;
+        KNN_HIP(hipMemcpyAsync(ix->stat + 11, &zero, sizeof(int), hipMemcpyHostToDevice, ix->stream));
+        KNN_HIP(hipStreamSynchronize(ix->stream));
         KNN_FAIL(KNN_EHIP, "certificate tail: a workgroup gave up waiting for the re-run plan "
                            "(error bits 0x%x); results of that search are not certified", acc[3]);
+    }
     *fallback_q = acc[0];
     if (first_fail) *first_fail = acc[2];
     if (ratio) std::memcpy(ratio, &acc[1], sizeof(float));

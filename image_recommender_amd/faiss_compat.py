@@ -200,6 +200,13 @@ class Index:
     def reserve(self, n: int) -> None:
         _lib.check(_lib.load().knn_reserve(self._h, int(n)), "knn_reserve")
 
+    def set_fence_mode(self, lazy: bool) -> None:
+        """Cross-stream fence of the *_device calls (include/imgrec_knn.h knn_set_fence_mode):
+        lazy=True records no event while every call uses one stream, which must then stay valid
+        until the next call on the index."""
+        mode = _lib.KNN_FENCE_LAZY if lazy else _lib.KNN_FENCE_EAGER
+        _lib.check(_lib.load().knn_set_fence_mode(self._h, mode), "knn_set_fence_mode")
+
     # -- search arithmetic (extension; include/imgrec_knn.h knn_search_mode) -------------------
     SEARCH_MODES = {"auto": _lib.KNN_SEARCH_AUTO, "exact": _lib.KNN_SEARCH_EXACT,
                     "split": _lib.KNN_SEARCH_SPLIT, "bf16": _lib.KNN_SEARCH_BF16,

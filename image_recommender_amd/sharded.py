@@ -168,15 +168,24 @@ class ShardedIndex:
         else:
             self.index.add(np.asarray(x, dtype=np.float32))
 
-    def search(self, q, k: int):
-        """q: (nq, d) float32 device tensor, identical on every rank -> (D, I) on every rank."""
+    def search(self, q, k: int, events=None):
+        """q: (nq, d) float32 device tensor, identical on every rank -> (D, I) on every rank.
+
+        events: optional 4 torch.cuda.Event recorded on the search stream before the local search,
+        after it, after the all-gather and after the merge (bench.py's per-rank phase times; each
+        record costs a few us of GPU time, so timed regions leave it None)."""
         import torch
         nq = q.shape[0]
-        st = torch.cuda.current_stream(q.device).cuda_stream
+        cs = torch.cuda.current_stream(q.device)
+        st = cs.cuda_stream
+        mark = (lambda i: events[i].record(cs)) if events is not None else (lambda i: None)
         if self.world == 1:
             D = torch.empty((nq, k), dtype=torch.float32, device=q.device)
             I = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+            mark(0)
             self.index.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
+            for i in (1, 2, 3):
+                mark(i)
             return D, I
         # the shard searches its query slice straight into its packed chunk; one all-gather moves
         # keys and labels (chunk and gather buffers are kept per (nq, k): every call is
@@ -191,13 +200,19 @@ class ShardedIndex:
             self._packed = {key: (buf, g) + packed_views(buf, nql, k)}
         buf, g, D, I = self._packed[key]
         ql = ql.contiguous()
+        mark(0)
         self.index.search_device(ql.data_ptr(), nql, k, D.data_ptr(), I.data_ptr(), st)
+        mark(1)
         gather_packed(buf, self.group, out=g)
+        mark(2)
         if not per:      # every slice searched the whole batch: group 0's row-shard chunks
-            return merge_packed_device(g[:self.rshards], nq, k, k, self.metric, st)
+            out = merge_packed_device(g[:self.rshards], nq, k, k, self.metric, st)
+            mark(3)
+            return out
         Do = torch.empty((nq, k), dtype=torch.float32, device=q.device)
         Io = torch.empty((nq, k), dtype=torch.int64, device=q.device)
         for s in range(self.query_groups):   # slice s: chunks s*R .. s*R + R - 1
             merge_packed_device(g[s * self.rshards:(s + 1) * self.rshards], per, k, k, self.metric,
                                 st, out=(Do[s * per:(s + 1) * per], Io[s * per:(s + 1) * per]))
+        mark(3)
         return Do, Io

@@ -7,10 +7,22 @@ Contract: for every query row
   3. every returned label's exact distance is within tol of the returned distance;
   4. labels equal the oracle's exactly at every rank whose oracle distance is separated from its
      neighbours' by more than 2*tol (ranks inside a tie window may permute).
+
+check_knn_tight adds the integer-exact label claim of north_star at an EMPIRICAL tie window
+(VERDICT r03 item 1): the window is a stated multiple of the largest |fp32 key - float64 key|
+actually measured over the returned pairs (this build's and, when given, the faiss-restated fp32
+oracle's), about 1e-6 of the key scale instead of the rigorous ~1e-4.  At every rank separated from
+its neighbours by more than that window the labels must equal the float64 oracle's AND the
+faiss-restated fp32 oracle's (oracle.flat_knn.search_blas_fp32_blocked = faiss's
+exhaustive_L2sqr_blas), and the top-k label SET must equal both wherever the k-th / (k+1)-th
+float64 gap exceeds it.  The fraction of ranks / sets so checked is returned and printed.
 """
 import numpy as np
 
 from oracle.flat_knn import fp32_error_bound, search_exact
+
+WINDOW_MULT = 8.0        # empirical window = WINDOW_MULT x the measured max |fp32 - float64|
+WINDOW_REL_FLOOR = 1e-6  # ... and at least this fraction of the query's key scale
 
 
 def _pair_bound(xb, xq, qi, ids, metric):
@@ -70,3 +82,59 @@ def check_knn(D, I, xb, xq, k, metric="l2", min_exact_frac=0.0, oracle=None):
     if total:
         assert checked / total >= min_exact_frac, (checked, total)
     return checked, total
+
+
+def check_knn_tight(D, I, xb, xq, k, metric="l2", oracle=None, blas=None, min_rank_frac=0.0,
+                    min_set_frac=0.0, tag=""):
+    """check_knn's rigorous checks, then integer-exact labels at the empirical window (module doc).
+
+    oracle: float64 (Dg, Ig) with k + 1 columns (search_exact); blas: the faiss-restated fp32
+    result (Db, Ib) of the same queries (search_blas_fp32_blocked), or None.
+    Returns {"rank_frac", "set_frac", "err", "window_rel", ...} and prints it."""
+    check_knn(D, I, xb, xq, k, metric, 0.0, oracle)
+    D = np.asarray(D, dtype=np.float64)
+    I = np.asarray(I)
+    Dg, Ig = oracle if oracle is not None else search_exact(xb, xq, k + 1, metric)
+    nq = xq.shape[0]
+    nv = min(k, xb.shape[0])
+    ex = np.stack([_exact_pair(xb, xq, q, I[q, :nv], metric) for q in range(nq)])
+    err = float(np.abs(ex[:, :nv] - D[:, :nv]).max())
+    err_blas = 0.0
+    if blas is not None:
+        Db, Ib = np.asarray(blas[0], np.float64), np.asarray(blas[1])
+        exb = np.stack([_exact_pair(xb, xq, q, Ib[q, :nv], metric) for q in range(nq)])
+        err_blas = float(np.abs(exb - Db[:, :nv]).max())
+    E = max(err, err_blas)
+    rank_ok = rank_tot = set_ok = set_tot = 0
+    worst_rel = 0.0
+    for q in range(nq):
+        gd = Dg[q]
+        scale = float(np.abs(gd[:nv + 1][Ig[q, :nv + 1] >= 0]).max()) + 1e-30
+        w = max(WINDOW_MULT * E, WINDOW_REL_FLOOR * scale)
+        worst_rel = max(worst_rel, w / scale)
+        for j in range(nv):
+            rank_tot += 1
+            lo = j == 0 or abs(gd[j] - gd[j - 1]) > w
+            hi = j + 1 >= len(gd) or Ig[q, j + 1] < 0 or abs(gd[j + 1] - gd[j]) > w
+            if lo and hi:
+                rank_ok += 1
+                assert I[q, j] == Ig[q, j], (tag, "float64", q, j, I[q], Ig[q], w)
+                if blas is not None:
+                    assert Ib[q, j] == Ig[q, j], (tag, "fp32 blas", q, j, Ib[q], Ig[q], w)
+        if nv < xb.shape[0]:
+            set_tot += 1
+            if Ig[q, nv] < 0 or abs(gd[nv] - gd[nv - 1]) > w:
+                set_ok += 1
+                want = set(Ig[q, :nv].tolist())
+                assert set(I[q, :nv].tolist()) == want, (tag, "top-k set", q, I[q], Ig[q])
+                if blas is not None:
+                    assert set(Ib[q, :nv].tolist()) == want, (tag, "blas top-k set", q, Ib[q], Ig[q])
+    res = {"rank_frac": rank_ok / max(rank_tot, 1), "set_frac": set_ok / max(set_tot, 1),
+           "ranks": rank_tot, "sets": set_tot, "err": err, "err_blas": err_blas,
+           "window_rel_max": worst_rel}
+    print(f"[tight {tag}] labels checked at {res['rank_frac']:.4f} of {rank_tot} ranks, top-k sets "
+          f"at {res['set_frac']:.4f} of {set_tot}; max |fp32 - fp64| {err:.3g} (blas {err_blas:.3g}), "
+          f"window <= {worst_rel:.3g} of the key scale")
+    assert res["rank_frac"] >= min_rank_frac, (tag, res)
+    assert res["set_frac"] >= min_set_frac, (tag, res)
+    return res

@@ -212,3 +212,124 @@ def test_multi_device_add_device_and_reset(faiss):
     multi.add(xb[:100])
     D, I = multi.search(xq, 5)
     check_knn(D, I, xb[:100], xq, 5, "l2")
+
+
+# --------------------------------------------------------------------------------------------
+# round 4: the cross-device branches of knn_multi.cpp on one GPU, the
+# exact re-run workspace on a device with few CUs and the fence on destroyed streams
+# --------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["auto", "exact"])
+def test_multi_device_forced_remote_staging(faiss, mode, monkeypatch):
+    """IMGREC_MULTI_FORCE_REMOTE=1: shards on the first device take the other devices' path —
+    rows staged by a peer copy into the shard's buffer before its add, queries peer-copied to
+    each shard, per-shard results peer-copied back into the gather buffer on devices[0] — so one
+    GPU runs the code an 8-GPU process runs.  Device adds, searches of 1 and 1024 queries at
+    k = 10 and k = 200 (the k > 32 merge), reset and re-add, against the oracle and one index."""
+    import torch
+    monkeypatch.setenv("IMGREC_MULTI_FORCE_REMOTE", "1")
+    d = 320
+    xb = mixture(24001, d, centres=60, seed=91)
+    xq = mixture(1024, d, centres=60, seed=92)
+    multi = faiss.IndexFlatL2(d, devices=[0, 0, 0])
+    monkeypatch.delenv("IMGREC_MULTI_FORCE_REMOTE")      # read at creation: this index keeps it
+    multi.search_mode = mode
+    t = torch.from_numpy(xb).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    multi.add_device(t[:10001].data_ptr(), 10001, st)
+    multi.add_device(t[10001:].data_ptr(), 24001 - 10001, st)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(multi.reconstruct_n(0, 24001), xb)
+    one = faiss.IndexFlatL2(d)
+    one.add(xb)
+    one.search_mode = mode
+    from oracle.flat_knn import search_exact
+    for nq, k in ((1, 10), (1024, 10), (1, 200), (1024, 200)):
+        q = torch.from_numpy(xq[:nq]).cuda()
+        D = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+        I = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+        multi.search_device(q.data_ptr(), nq, k, D.data_ptr(), I.data_ptr(), st)
+        torch.cuda.synchronize()
+        Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
+        sel = np.arange(0, nq, 41)
+        check_knn(Dh[sel], Ih[sel], xb, xq[sel], k, "l2", min_exact_frac=0.5,
+                  oracle=search_exact(xb, xq[sel], k + 1, "l2"))
+        D2, I2 = multi.search(xq[:nq], k)                            # host entry point
+        np.testing.assert_array_equal(I2, Ih)
+        D1, I1 = one.search(xq[:nq], k)
+        assert (I1 == Ih).mean() > 0.99, (nq, k)    # (k > 32: GEMM blocking differs per shard)
+    multi.reset()
+    assert multi.ntotal == 0
+    multi.add_device(t[:500].data_ptr(), 500, st)
+    D, I = multi.search(xq[:7], 5)
+    check_knn(D, I, xb[:500], xq[:7], 5, "l2")
+
+
+def test_exact_rerun_with_few_cus(faiss, monkeypatch):
+    """IMGREC_CUS=8 plans every launch for 8 CUs (a partitioned device): the certificate tail's
+    grid is 8 workgroups, and 1100 all-tied queries (35 query blocks of 32 > 8) need the exact
+    re-run's lists sized by the query count, not by the grid (the grid-sized buffer
+    overflowed there)."""
+    monkeypatch.setenv("IMGREC_CUS", "8")
+    dup, nq = 1100, 1100
+    base = mixture(150, 256, centres=20, seed=9)
+    xb = np.repeat(base, dup, axis=0)
+    src = np.arange(nq) % 150
+    xq = base[src] + np.float32(1e-3)
+    idx = faiss.IndexFlatL2(256)
+    monkeypatch.delenv("IMGREC_CUS")
+    idx.add(xb)
+    idx.search_mode = "bf16"
+    D, I = idx.search(xq, 10)
+    st = idx.certificate_stats()
+    assert st["candidate_queries"] == nq and st["exact_reruns"] == nq
+    assert (I == src[:, None] * dup + np.arange(10)[None, :]).all()
+    check_knn(D[:40], I[:40], xb, xq[:40], 10, "l2")
+
+
+def _hip():
+    import ctypes as C
+    import torch  # noqa: F401  (its HIP runtime is the one libimgrec.so binds)
+    return C.CDLL("libamdhip64.so.7", mode=C.RTLD_GLOBAL)   # by SONAME: the runtime already loaded
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_fence_across_destroyed_and_switched_streams(faiss, lazy):
+    """Default (eager) fence: a search on a stream the caller destroys right after the call, then
+    a search on another stream and the stats read — ordered, no error (the lazy record
+    on a destroyed stream wedged the index).  Lazy fence: back-to-back searches on one stream,
+    then a switch to a live stream, equal the eager results."""
+    import ctypes as C
+    import torch
+    hip = _hip()
+    d = 256
+    xb = mixture(20000, d, centres=40, seed=31)
+    xq = mixture(300, d, centres=40, seed=32)
+    idx = faiss.IndexFlatL2(d)
+    idx.set_fence_mode(lazy)
+    idx.add(xb)
+    q = torch.from_numpy(xq).cuda()
+    outs = []
+    for _ in range(3):
+        D = torch.empty((300, 10), dtype=torch.float32, device="cuda")
+        I = torch.empty((300, 10), dtype=torch.int64, device="cuda")
+        outs.append((D, I))
+    torch.cuda.synchronize()
+    if not lazy:
+        s = C.c_void_p()
+        assert hip.hipStreamCreate(C.byref(s)) == 0
+        idx.search_device(q.data_ptr(), 300, 10, outs[0][0].data_ptr(), outs[0][1].data_ptr(), s.value)
+        assert hip.hipStreamDestroy(s) == 0
+    else:
+        st = torch.cuda.current_stream().cuda_stream
+        idx.search_device(q.data_ptr(), 300, 10, outs[0][0].data_ptr(), outs[0][1].data_ptr(), st)
+        idx.search_device(q.data_ptr(), 300, 10, outs[1][0].data_ptr(), outs[1][1].data_ptr(), st)
+    other = torch.cuda.Stream()
+    idx.search_device(q.data_ptr(), 300, 10, outs[2][0].data_ptr(), outs[2][1].data_ptr(),
+                      other.cuda_stream)
+    other.synchronize()
+    idx.certificate_stats()                                  # host read after the switch
+    torch.cuda.synchronize()
+    I0, I2 = outs[0][1].cpu().numpy(), outs[2][1].cpu().numpy()
+    np.testing.assert_array_equal(I0, I2)
+    np.testing.assert_array_equal(outs[0][0].cpu().numpy(), outs[2][0].cpu().numpy())
+    check_knn(outs[2][0].cpu().numpy()[::10], I2[::10], xb, xq[::10], 10, "l2", min_exact_frac=0.5)

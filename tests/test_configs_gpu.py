@@ -18,15 +18,23 @@ oracle.flat_knn.search_exact (float64, host, streamed block by block):
   itself at rank 0.
 
 Data come from bench.py's own block-seeded device generators, so they are the bench's rows.
+
+Every full-size check also runs tests/knn_check.check_knn_tight: labels
+integer-exact against the float64 oracle AND against faiss IndexFlatL2's fp32 arithmetic restated
+(oracle.flat_knn.search_blas_fp32_blocked, exhaustive_L2sqr_blas) at every rank separated by more
+than an empirical window (8x the measured max |fp32 - float64| key error, ~1e-6 of the key scale),
+and top-k label sets equal wherever the k-th / (k+1)-th gap exceeds it; the checked fractions are
+printed and held to stated minimums.
 """
 import numpy as np
 import pytest
 
-from tests.knn_check import check_knn
+from tests.knn_check import check_knn, check_knn_tight
 
 pytestmark = pytest.mark.gpu
 
 NQ, K, NCHECK = 1024, 10, 32
+RANK_FRAC, SET_FRAC = 0.95, 0.9      # minimum fractions of ranks / top-k sets label-checked
 
 
 @pytest.fixture(scope="module")
@@ -57,7 +65,7 @@ def _generate(torch, cfg_id, r0, r1, nq):
 def cfg3(faiss):
     """The cfg3 corpus resident in one index + the oracle of the sampled queries (computed once)."""
     import torch
-    from oracle.flat_knn import search_exact
+    from oracle.flat_knn import search_blas_fp32_blocked, search_exact
     blocks, xb, q = _generate(torch, 3, 0, 1_000_000, NQ)
     idx = faiss.IndexFlatL2(xb.shape[1])
     idx.reserve(xb.shape[0])
@@ -69,7 +77,8 @@ def cfg3(faiss):
     sel = np.linspace(0, NQ - 1, NCHECK).astype(int)
     xq = q.cpu().numpy()
     oracle = search_exact(xb, xq[sel], K + 1, "l2")
-    return dict(idx=idx, xb=xb, q=q, xq=xq, sel=sel, oracle=oracle)
+    blas = search_blas_fp32_blocked(xb, xq[sel], K)
+    return dict(idx=idx, xb=xb, q=q, xq=xq, sel=sel, oracle=oracle, blas=blas)
 
 
 def test_cfg3_full_size_auto_bf16(faiss, cfg3):
@@ -94,6 +103,9 @@ def test_cfg3_full_size_auto_bf16(faiss, cfg3):
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     check_knn(Dh[sel], Ih[sel], cfg3["xb"], cfg3["xq"][sel], K, "l2", min_exact_frac=0.5,
               oracle=cfg3["oracle"])
+    check_knn_tight(Dh[sel], Ih[sel], cfg3["xb"], cfg3["xq"][sel], K, "l2", oracle=cfg3["oracle"],
+                    blas=cfg3["blas"], min_rank_frac=RANK_FRAC, min_set_frac=SET_FRAC,
+                    tag="cfg3 bf16 nq=1024")
     # the host entry point (the faiss call the reference makes) returns the same result
     D2, I2 = idx.search(cfg3["xq"], K)
     np.testing.assert_array_equal(I2, Ih)
@@ -107,6 +119,8 @@ def test_cfg3_full_size_single_queries_int8(faiss, cfg3):
     from image_recommender_amd import _lib
     idx, xq = cfg3["idx"], cfg3["xq"]
     Dg, Ig = cfg3["oracle"]
+    Db, Ib = cfg3["blas"]
+    rows, Ds, Is = [], [], []
     for r in range(0, len(cfg3["sel"]), 2):
         s = cfg3["sel"][r]
         D, I = idx.search(xq[s:s + 1], K)
@@ -116,12 +130,19 @@ def test_cfg3_full_size_single_queries_int8(faiss, cfg3):
         assert 0.0 <= st["max_err_over_bound"] < 1.0
         check_knn(D, I, cfg3["xb"], xq[s:s + 1], K, "l2", min_exact_frac=0.5,
                   oracle=(Dg[r:r + 1], Ig[r:r + 1]))
+        rows.append(r), Ds.append(D), Is.append(I)
     for r in range(0, len(cfg3["sel"]) - 1, 4):
         pair = cfg3["sel"][[r, r + 1]]
         D, I = idx.search(xq[pair], K)
         assert _lib.load().knn_last_path(idx.handle) == 3
         check_knn(D, I, cfg3["xb"], xq[pair], K, "l2", min_exact_frac=0.5,
                   oracle=(Dg[r:r + 2], Ig[r:r + 2]))
+        rows += [r, r + 1]
+        Ds.append(D), Is.append(I)
+    rows = np.array(rows)
+    check_knn_tight(np.concatenate(Ds), np.concatenate(Is), cfg3["xb"], xq[cfg3["sel"][rows]], K,
+                    "l2", oracle=(Dg[rows], Ig[rows]), blas=(Db[rows], Ib[rows]),
+                    min_rank_frac=RANK_FRAC, min_set_frac=SET_FRAC, tag="cfg3 int8 nq=1,2")
 
 
 def test_cfg3_full_size_exact_kernel(faiss, cfg3):
@@ -136,6 +157,10 @@ def test_cfg3_full_size_exact_kernel(faiss, cfg3):
     Dg, Ig = cfg3["oracle"]
     rows = [list(cfg3["sel"]).index(s) for s in sel]
     check_knn(D, I, cfg3["xb"], xq[sel], K, "l2", min_exact_frac=0.5, oracle=(Dg[rows], Ig[rows]))
+    Db, Ib = cfg3["blas"]
+    check_knn_tight(D, I, cfg3["xb"], xq[sel], K, "l2", oracle=(Dg[rows], Ig[rows]),
+                    blas=(Db[rows], Ib[rows]), min_rank_frac=RANK_FRAC, min_set_frac=SET_FRAC,
+                    tag="cfg3 exact fp32")
 
 
 def test_cfg4_rank_shape_eight_shards_packed_merge(faiss, cfg3):
@@ -169,6 +194,9 @@ def test_cfg4_rank_shape_eight_shards_packed_merge(faiss, cfg3):
     Dh, Ih = D.cpu().numpy(), I.cpu().numpy()
     check_knn(Dh[sel], Ih[sel], xb, cfg3["xq"][sel], K, "l2", min_exact_frac=0.5,
               oracle=cfg3["oracle"])
+    check_knn_tight(Dh[sel], Ih[sel], xb, cfg3["xq"][sel], K, "l2", oracle=cfg3["oracle"],
+                    blas=cfg3["blas"], min_rank_frac=RANK_FRAC, min_set_frac=SET_FRAC,
+                    tag="cfg4 8 x 125k packed merge")
     D1, I1 = cfg3["idx"].search(cfg3["xq"], K)
     print(f"8 shards: {fallbacks} certificate fallbacks; labels equal to one index: "
           f"{(Ih == I1).mean():.5f}")
@@ -183,7 +211,7 @@ def test_cfg4_last_rank_shard_full_size(faiss):
     """One 1.25M-row shard of the 10M x 1968 corpus (rank 7 of 8: rows 8.75M..10M, labels offset
     by 8.75M), 1024 queries on AUTO; sampled queries against the oracle on that shard."""
     import torch
-    from oracle.flat_knn import search_exact
+    from oracle.flat_knn import search_blas_fp32_blocked, search_exact
     r0, r1 = 8_750_000, 10_000_000
     blocks, xb, q = _generate(torch, 4, r0, r1, NQ)
     sh = faiss.IndexFlatL2(xb.shape[1])
@@ -203,8 +231,11 @@ def test_cfg4_last_rank_shard_full_size(faiss):
     xq = q.cpu().numpy()[sel]
     Ih = I.cpu().numpy()[sel]
     assert (Ih >= r0).all() and (Ih < r1).all()
-    check_knn(D.cpu().numpy()[sel], Ih - r0, xb, xq, K, "l2", min_exact_frac=0.5,
-              oracle=search_exact(xb, xq, K + 1, "l2"))
+    oracle = search_exact(xb, xq, K + 1, "l2")
+    check_knn(D.cpu().numpy()[sel], Ih - r0, xb, xq, K, "l2", min_exact_frac=0.5, oracle=oracle)
+    check_knn_tight(D.cpu().numpy()[sel], Ih - r0, xb, xq, K, "l2", oracle=oracle,
+                    blas=search_blas_fp32_blocked(xb, xq, K), min_rank_frac=RANK_FRAC,
+                    min_set_frac=SET_FRAC, tag="cfg4 1.25M-row shard")
 
 
 def test_cfg5_pipeline_smoke(gpu):
@@ -260,7 +291,7 @@ def test_cfg2_full_size_auto_with_forced_rerun(faiss):
     import torch
     from image_recommender_amd import _lib
     from oracle import c_oracle
-    from oracle.flat_knn import search_exact
+    from oracle.flat_knn import search_blas_fp32_blocked, search_exact
     blocks, xb, q = _generate(torch, 2, 0, 1_000_000, NQ)
     assert xb.shape == (1_000_000, 768)
     src = xb[_DUP_SRC].copy()
@@ -292,8 +323,13 @@ def test_cfg2_full_size_auto_with_forced_rerun(faiss):
     assert (Dh[0] == 0.0).all()
     xq = q.cpu().numpy()
     sel = np.linspace(0, NQ - 1, NCHECK).astype(int)
-    check_knn(Dh[sel], Ih[sel], xb, xq[sel], K, "l2", min_exact_frac=0.5,
-              oracle=search_exact(xb, xq[sel], K + 1, "l2"))
+    oracle = search_exact(xb, xq[sel], K + 1, "l2")
+    check_knn(Dh[sel], Ih[sel], xb, xq[sel], K, "l2", min_exact_frac=0.5, oracle=oracle)
+    # (query 0's ten answers are exact copies, tied at 0: inside any window by construction)
+    check_knn_tight(Dh[sel], Ih[sel], xb, xq[sel], K, "l2", oracle=oracle,
+                    blas=search_blas_fp32_blocked(xb, xq[sel], K),
+                    min_rank_frac=RANK_FRAC * (NCHECK - 1) / NCHECK,
+                    min_set_frac=SET_FRAC * (NCHECK - 1) / NCHECK, tag="cfg2 bf16 nq=1024")
     Dc, Ic = c_oracle.flat_search(xb, xq[sel[:8]], K + 1, "l2")
     check_knn(Dh[sel[:8]], Ih[sel[:8]], xb, xq[sel[:8]], K, "l2", min_exact_frac=0.5, oracle=(Dc, Ic))
 
@@ -304,8 +340,10 @@ def test_cfg2_full_size_auto_with_forced_rerun(faiss):
 def _device_oracle(torch, cfg_id, nrows, qs, k, need):
     """float64 exact top-(k) of the queries qs (device tensor) over rows [0, nrows) of bench
     config cfg_id, regenerated block by block on the device (bench.gen_rows: the same rows the
-    index holds), keeping the row vectors of the running top-k and of every label in `need`.
-    Returns (D float64, I int64, {label: float32 row})."""
+    index holds), keeping the row vectors of the running top-k and of every label in `need`; and
+    the top-(k - 1) by faiss IndexFlatL2's fp32 key form (|q|^2 + |x|^2 - 2 q.x, fp32 GEMM per
+    block, exhaustive_L2sqr_blas restated on the device).
+    Returns (D float64, I int64, {label: float32 row}, (D fp32, I fp32-ranked))."""
     import bench
     cfg = dict(bench.CONFIGS[cfg_id])
     dev = qs.device
@@ -318,8 +356,21 @@ def _device_oracle(torch, cfg_id, nrows, qs, k, need):
     bv = torch.zeros((nq, k, d), dtype=torch.float32, device=dev)
     need_t = torch.tensor(sorted(need), dtype=torch.int64, device=dev)
     rows, pos = {}, 0
+    q32 = qs.float()
+    qn32 = (q32 * q32).sum(1, keepdim=True)
+    kb = k - 1
+    fd = torch.full((nq, kb), float("inf"), dtype=torch.float32, device=dev)
+    fi = torch.full((nq, kb), -1, dtype=torch.int64, device=dev)
+    fv = torch.zeros((nq, kb, d), dtype=torch.float32, device=dev)
     for blk in bench.gen_rows(torch, cfg, centres, 0, nrows, dev, cfg_id):
         n = blk.shape[0]
+        d32 = ((qn32 + (blk * blk).sum(1)[None, :]) - 2.0 * (q32 @ blk.T)).clamp_min_(0.0)
+        v32, i32 = torch.topk(d32, min(kb, n), dim=1, largest=False)
+        c32, ci32 = torch.cat([fd, v32], 1), torch.cat([fi, i32 + pos], 1)
+        cv32 = torch.cat([fv, blk[i32]], 1)
+        o32 = torch.topk(c32, kb, dim=1, largest=False).indices
+        fd, fi = torch.gather(c32, 1, o32), torch.gather(ci32, 1, o32)
+        fv = torch.gather(cv32, 1, o32[:, :, None].expand(-1, -1, d))
         xd = blk.double()
         dd = (qn + (xd * xd).sum(1)[None, :] - 2.0 * (qd @ xd.T)).clamp_min_(0.0)
         v, i = torch.topk(dd, min(k, n), dim=1, largest=False)
@@ -339,7 +390,9 @@ def _device_oracle(torch, cfg_id, nrows, qs, k, need):
     for qi in range(nq):
         for j in range(k):
             rows[int(bi[qi, j])] = bv[qi, j].cpu().numpy()
-    return bd.cpu().numpy(), bi.cpu().numpy(), rows
+        for j in range(kb):
+            rows[int(fi[qi, j])] = fv[qi, j].cpu().numpy()
+    return bd.cpu().numpy(), bi.cpu().numpy(), rows, (fd.cpu().numpy(), fi.cpu().numpy())
 
 
 def test_cfg4_whole_10m_corpus_eight_shards(faiss):
@@ -373,12 +426,15 @@ def test_cfg4_whole_10m_corpus_eight_shards(faiss):
     sel = np.linspace(0, NQ - 1, 16).astype(int)
     Dh, Ih = D.cpu().numpy()[sel], I.cpu().numpy()[sel]
     assert (Ih >= 0).all() and (Ih < n).all()
-    Dg, Ig, rows = _device_oracle(torch, 4, n, q[sel], K + 1, set(Ih.ravel().tolist()))
+    Dg, Ig, rows, (Db, Ib) = _device_oracle(torch, 4, n, q[sel], K + 1, set(Ih.ravel().tolist()))
     labels = np.array(sorted(rows))
     xb = np.stack([rows[int(l)] for l in labels])
     remap = lambda a: np.searchsorted(labels, a)                 # noqa: E731
     check_knn(Dh, remap(Ih), xb, q.cpu().numpy()[sel], K, "l2", min_exact_frac=0.5,
               oracle=(Dg, remap(Ig)))
+    check_knn_tight(Dh, remap(Ih), xb, q.cpu().numpy()[sel], K, "l2", oracle=(Dg, remap(Ig)),
+                    blas=(Db, remap(Ib)), min_rank_frac=RANK_FRAC, min_set_frac=SET_FRAC,
+                    tag="cfg4 whole 10M, 8 shards")
     hits = sum(len(set(a.tolist()) & set(b[:K].tolist())) for a, b in zip(Ih, Ig))
     assert hits / (K * len(sel)) == 1.0, hits                    # recall@10 on the sample
     del idx

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from tests.datagen import concat_rows, mixture
-from tests.knn_check import check_knn
+from tests.knn_check import check_knn, check_knn_tight
 
 pytestmark = pytest.mark.gpu
 
@@ -55,9 +55,14 @@ def test_i8_l2_shapes(faiss, d, nq):
     D, I = idx.search(xq, 10)
     assert _lib().knn_last_path(idx.handle) == 3
     _stats(idx, nq)
-    # (at d >= 1024 the mixture's neighbours crowd inside the fp32 tie window: fewer ranks are
-    # tie-free, every label is still checked against its exact distance)
+    # (at d >= 1024 the mixture's neighbours crowd inside the RIGOROUS fp32 window (~1e-4 of the
+    # key): check_knn_tight checks the labels at the empirical ~1e-6 window, against the float64
+    # oracle and faiss's fp32 form)
     check_knn(D, I, xb, xq, 10, "l2", min_exact_frac=0.5 if d < 1024 else 0.25)
+    if d >= 1024:
+        from oracle.flat_knn import search_blas_fp32_blocked
+        check_knn_tight(D, I, xb, xq, 10, "l2", blas=search_blas_fp32_blocked(xb, xq, 10),
+                        min_rank_frac=0.95, min_set_frac=1.0, tag=f"i8 d={d} nq={nq}")
 
 
 @pytest.mark.parametrize("k", [1, 5, 10, 16, 17, 32])
@@ -222,9 +227,11 @@ def test_i8_wide_rows_and_list_depths(faiss, d, nq, k):
     D, I = idx.search(xq, k)
     assert _lib().knn_last_path(idx.handle) == 3
     _stats(idx, nq)
-    # (at these widths the mixture's neighbours sit inside the fp32 tie window: every returned
-    # label's exact distance and every rank's distance are still checked against the oracle)
-    check_knn(D, I, xb, xq, k, "l2", min_exact_frac=0.0)
+    # (at these widths the mixture's neighbours sit inside the RIGOROUS fp32 window: the labels
+    # are checked at the empirical window instead, against float64 and faiss's fp32 form)
+    from oracle.flat_knn import search_blas_fp32_blocked
+    check_knn_tight(D, I, xb, xq, k, "l2", blas=search_blas_fp32_blocked(xb, xq, k),
+                    min_rank_frac=0.95, min_set_frac=0.5, tag=f"i8 wide d={d} nq={nq} k={k}")
 
 
 def test_i8_mode_refused_outside_its_dimensions(faiss):
