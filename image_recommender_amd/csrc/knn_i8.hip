@@ -19,7 +19,8 @@
 // Scan: one workgroup per row split (8-row groups s, s + nsplit, ... as the bf16 kernels, so a
 // store with similar images on adjacent rows spreads them over every split), four waves; a wave
 // takes one 8-row group at a time, a 16-lane group per row, lane j the 64-element blocks j,
-// j + 16, ... of its row: 16-B code loads (two register sets: the next group's loads in flight),
+// j + 16, ... of its row (rows stored without padding: knn_kernels.h i8_slot): 16-B code loads
+// (two register sets: the next group's loads in flight),
 // the query's codes from LDS, exact int32 v_dot4_i32_i8 products of the row's codes with the
 // query's hi and lo codes (no int8 -> fp32 conversions: 0.56 VALU instructions per element and
 // query, against 2 for an fp32 FMA form that converts every code), one fp32 fold per block
@@ -59,9 +60,9 @@ __device__ __forceinline__ float row16_sum(float v) {
     return v;
 }
 
-// Build: one wave per row, lane b quantises block b (nblk <= 64); rows padded to whole 16-block
-// groups with zero codes (the build zero-fills the slots of blocks >= nblk: see launch_i8_rows).  The residual norm is computed
-// against the dequantised value the scan uses (s * c) and inflated for its own fp32 evaluation.
+// Build: one wave per row, lane b quantises block b (nblk <= 64) into its slots of the compact
+// row (i8_slot).  The residual norm is computed against the dequantised value the scan uses
+// (s * c) and inflated for its own fp32 evaluation.
 __global__ void __launch_bounds__(256)
 i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t* __restrict__ codes,
                float* __restrict__ scales, float* __restrict__ resid) {
@@ -96,17 +97,12 @@ i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t
             }
             w[e4] = word;
         }
-        // chunk c of block b at 16-B slot 16 (4 (b / 16) + c) + b % 16 of the row (i8_row_bytes)
-        uint4* dst = reinterpret_cast<uint4*>(codes + row * (int64_t)i8_row_bytes(nblk)) +
-                     64 * (lane >> 4) + (lane & 15);
+        // chunk c of block b at 16-B slot i8_slot(nblk, b, c) of the row (knn_kernels.h)
+        uint4* dst = reinterpret_cast<uint4*>(codes + row * (int64_t)i8_row_bytes(nblk));
 #pragma unroll
-        for (int c = 0; c < 4; ++c) dst[16 * c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+        for (int c = 0; c < 4; ++c)
+            dst[i8_slot(nblk, lane, c)] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
         scales[row * nblk + lane] = s;
-    } else if (lane < 16 * ((nblk + 15) / 16)) {      // the padding slots of the last group
-        uint4* dst = reinterpret_cast<uint4*>(codes + row * (int64_t)i8_row_bytes(nblk)) +
-                     64 * (lane >> 4) + (lane & 15);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) dst[16 * c] = make_uint4(0u, 0u, 0u, 0u);
     }
     rsq = wave_sum(rsq);
     xsq = wave_sum(xsq);
@@ -324,17 +320,22 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
 #pragma unroll
             for (int bi = 0; bi < NBI; ++bi) {
                 const int b = j + 16 * bi;
-                // chunk c of block b: slot 16 (4 bi + c) + j, so the 16 lanes of a row read 256
-                // contiguous bytes per load (slots of blocks >= nblk hold zeros)
+                // chunk c of block b: slot 64 bi + m c + j (i8_slot, m = blocks of this group), so
+                // the m live lanes of a row read 16 m contiguous bytes per load; lanes past nblk
+                // load nothing (zero codes, zero scale)
+                const int m = min(16, nblk - 16 * bi);
                 const uint4* src = reinterpret_cast<const uint4*>(codes + (int64_t)rc * rowb) + 64 * bi + j;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    if constexpr (kNtCodes) {    // streamed once per search: non-temporal loads
-                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                        const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 16 * c));
-                        G.cw[h][bi][c] = make_uint4(w.x, w.y, w.z, w.w);
-                    } else {
-                        G.cw[h][bi][c] = src[16 * c];
+                    G.cw[h][bi][c] = make_uint4(0u, 0u, 0u, 0u);
+                    if (b < nblk) {
+                        if constexpr (kNtCodes) {    // streamed once per search: non-temporal loads
+                            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                            const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + m * c));
+                            G.cw[h][bi][c] = make_uint4(w.x, w.y, w.z, w.w);
+                        } else {
+                            G.cw[h][bi][c] = src[m * c];
+                        }
                     }
                 }
                 G.sc[h][bi] = b < nblk ? scales[(int64_t)rc * nblk + b] : 0.f;

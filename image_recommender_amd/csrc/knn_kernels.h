@@ -182,9 +182,16 @@ struct I8Args {
     int64_t* cand_i;
     int ncand;
 };
-// bytes per row of the int8 copy: 16-block groups of 1 KiB, block b's 4 chunks at 16-B slots
-// 16 (4 (b / 16) + c) + b % 16 (one contiguous 256-B load per 16-lane row group in the scan)
-__host__ __device__ inline int64_t i8_row_bytes(int nblk) { return (int64_t)1024 * ((nblk + 15) / 16); }
+// Bytes per row of the int8 copy: 64 per block, no padding (round 4; rows were whole 1-KiB
+// groups of 16 blocks, 25 % zeros at d = 768).  Blocks sit in groups of 16 (the scan's 16 lanes of
+// a row): group g = b / 16 holds m = min(16, nblk - 16 g) blocks at byte 1024 g, chunk c (16 B)
+// of its block j = b % 16 at 16-B slot m c + j, so lane j's load c of a row reads 16 m contiguous
+// bytes with its group's other lanes (256 B for a full group).
+__host__ __device__ inline int64_t i8_row_bytes(int nblk) { return (int64_t)64 * nblk; }
+__host__ __device__ inline int i8_slot(int nblk, int b, int c) {
+    const int g = b >> 4, m = nblk - 16 * g < 16 ? nblk - 16 * g : 16;
+    return 64 * g + m * c + (b & 15);
+}
 hipError_t launch_i8_rows(const float* xb, int64_t n, int dp, int nblk, int8_t* codes, float* scales,
                           float* resid, hipStream_t st);
 hipError_t launch_i8_scan(const I8Args& a, hipStream_t st);

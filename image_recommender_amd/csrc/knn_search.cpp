@@ -356,20 +356,20 @@ bool use_b16(const knn_index* ix, int64_t nq, int k) {
 // the bf16 copy's bytes; its dot products grow with the batch: nq <= 4 is HBM-bound, nq = 5-8
 // VALU-bound and still faster than the bf16 pass; one query on 1000-65536 rows 0.05-0.075 ms
 // against the exact kernel's 0.18-0.22, profiles/r03/small_corpora/)
-// The int8 rows sit in whole 1-KiB groups of 16 blocks, so below 9 blocks (d <= 512) a row
-// streams more bytes than its bf16 copy (d = 128: 1 KiB against 256 B; one query on 1M rows
-// 0.223 ms against the bf16 path's 0.162, profiles/r03/small_corpora/small_d.jsonl): AUTO takes
-// the int8 path there only while the copy is small enough (<= 64 MB, ~10 us of streaming) for
-// the fixed costs to decide.
+// A row's 16-lane group in the scan has one lane per 64-element block, so narrow rows leave most
+// lanes idle (d = 128: 2 of 16) and the scan stops being HBM-bound: below kI8MinBlocks blocks
+// AUTO takes the int8 path only while the copy is small enough (<= 64 MB, ~10 us of streaming)
+// for the fixed costs to decide (round 3 measured one query on 1M x 128 rows: int8 0.223 ms,
+// bf16 0.162, with the then-padded 1-KiB rows; profiles/r03/small_corpora/small_d.jsonl).
 constexpr int kI8AutoQ = 8;
+constexpr int kI8MinBlocks = 8;
 constexpr int64_t kI8SmallCopyBytes = 64ll << 20;
 bool use_i8(const knn_index* ix, int64_t nq, int k) {
     if (ix->nblk8 <= 0 || k > KNN_MAX_K || nq > kI8MaxQ) return false;
     if (ix->mode == KNN_SEARCH_I8) return true;
     if (ix->mode != KNN_SEARCH_AUTO || nq > kI8AutoQ) return false;
     const int64_t i8_row = i8_row_bytes(ix->nblk8) + 4 * ix->nblk8;
-    const int64_t b16_row = 2 * (int64_t)ix->dpb;
-    return !ix->b16_ok || i8_row <= b16_row || ix->ntotal * i8_row <= kI8SmallCopyBytes;
+    return !ix->b16_ok || ix->nblk8 >= kI8MinBlocks || ix->ntotal * i8_row <= kI8SmallCopyBytes;
 }
 
 bool use_split(const knn_index* ix, int64_t nq, int k) {

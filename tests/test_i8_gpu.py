@@ -104,8 +104,8 @@ def test_i8_concat_layout_self_query(faiss):
 
 
 def test_i8_auto_picks_int8_for_single_queries(faiss):
-    """AUTO: one to eight queries take the int8 path, nine the bf16 path; at d <= 512 (a row's
-    int8 group wider than its bf16 copy) only while the int8 copy is small."""
+    """AUTO: one to eight queries take the int8 path, nine the bf16 path; below 8 blocks per row
+    (d <= 448: most of a row's 16 scan lanes idle) only while the int8 copy is small."""
     d = 1024
     xb = mixture(140000, d, centres=200, seed=3)
     xq = mixture(9, d, centres=200, seed=4)
@@ -119,12 +119,12 @@ def test_i8_auto_picks_int8_for_single_queries(faiss):
         check_knn(D, I, xb, xq[:nq], 10, "l2", min_exact_frac=0.5,
                   oracle=(orc[0][:nq], orc[1][:nq]))
     del idx
-    narrow = faiss.IndexFlatL2(256)                          # 1 KiB int8 group vs 512-B bf16 row
-    xn = mixture(70000, 256, centres=100, seed=5)
-    narrow.add(xn[:30000])                                   # 31 MB int8 copy: int8
+    narrow = faiss.IndexFlatL2(256)                          # 4 blocks: 4 of 16 lanes live
+    xn = mixture(260000, 256, centres=100, seed=5)
+    narrow.add(xn[:30000])                                   # 8 MB int8 copy: int8
     narrow.search(xn[:1], 10)
     assert _lib().knn_last_path(narrow.handle) == 3
-    narrow.add(xn[30000:])                                   # 73 MB: bf16
+    narrow.add(xn[30000:])                                   # 71 MB: bf16
     D, I = narrow.search(xn[:1], 10)
     assert _lib().knn_last_path(narrow.handle) == 2
     assert I[0, 0] == 0

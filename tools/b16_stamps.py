@@ -16,15 +16,16 @@ from image_recommender_amd import _lib
 from image_recommender_amd.faiss_compat import METRIC_L2
 from image_recommender_amd.sharded import ShardedIndex
 
-cfg = dict(bench.CONFIGS[3])
+CFG = int(os.environ.get("IMGREC_STAMPS_CFG", "3"))    # bench config (2: 1M x 768)
+cfg = dict(bench.CONFIGS[CFG])
 if os.environ.get("IMGREC_STAMPS_ROWS"):       # e.g. 125000: the N = 8 shard
     cfg["rows"] = int(os.environ["IMGREC_STAMPS_ROWS"])
 dev = torch.device("cuda", 0)
 D = int(sum(cfg["parts"]))
-centres = bench.make_centres(torch, cfg, dev, 3)
-q = bench.gen_queries(torch, cfg, centres, 1024, dev, 3)
+centres = bench.make_centres(torch, cfg, dev, CFG)
+q = bench.gen_queries(torch, cfg, centres, 1024, dev, CFG)
 shard = ShardedIndex(D, cfg["rows"], METRIC_L2, device=0)
-for blk in bench.gen_rows(torch, cfg, centres, shard.row0, shard.row1, dev, 3):
+for blk in bench.gen_rows(torch, cfg, centres, shard.row0, shard.row1, dev, CFG):
     shard.add_local(blk)
 shard.index.search_mode = "bf16"
 for _ in range(4):

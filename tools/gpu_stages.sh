@@ -1,0 +1,74 @@
+#!/bin/bash
+# One GPU lease, several named stages run in order; each GPU step under its own timeout, the
+# script stops at the first failure (gpurun rules: no retries, nothing after a fault).
+#   tools/gpu_stages.sh TAG stage [stage ...]
+# stages:
+#   tests[=FILES]   pytest -m gpu (all, or the listed test files, comma-separated)
+#   smoke           __graft_entry__.smoke()
+#   bench           bench.py (default workload, CPU baseline included) -> bench.json
+#   bench2          bench.py --config 2 (1M x 768) -> bench_cfg2.json
+#   rows125k        bench.py --rows 125000 --profile-only (the N = 8 per-rank step) -> rows125k.json
+#   nq1             bench.py --nq 1 --profile-only, cfg3 and cfg2 -> nq1_cfg{3,2}.json
+#   rocprof         rocprofv3 --kernel-trace --stats of a bench run -> prof/
+#   rehearse=N      gloo N-rank rehearsal of bench.py on this one GPU -> rehearse_nN.json
+#   pmc[=ARGS]      clock/MFMA-busy and HBM-traffic passes of the candidate kernel (bench args,
+#                   comma-separated: pmc=--config,2)
+#   stamps=CFG      per-tile stage-loop / epilogue cycles of the 256 x 256 bf16 kernel on bench
+#                   config CFG (lib/libimgrec_stamps.so: tools/build_variants.sh stamps -DIMGREC_B16_STAMPS)
+# Extra bench arguments for every bench stage: BENCH_ARGS.
+set -u
+export PYTHONPATH=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
+TAG=$1; shift
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+BA=${BENCH_ARGS:-}
+fail() { echo "stage $1 failed"; tail -30 "$2"; exit 1; }
+for st in "$@"; do
+  name=${st%%=*}; arg=${st#*=}; [ "$arg" = "$st" ] && arg=""
+  echo "== $st $(date +%T)"
+  case $name in
+    tests)
+      files=tests; [ -n "$arg" ] && files=$(echo "$arg" | tr ',' ' ')
+      timeout -k 10 1000 python -u -m pytest $files -x -v -s -m gpu --timeout 300 --timeout-method thread \
+        > $OUT/pytest_$(echo "$arg" | tr ',/' '__' | cut -c1-40).log 2>&1 || fail tests $OUT/pytest_*.log
+      tail -2 $OUT/pytest_*.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || fail smoke $OUT/smoke.log
+      tail -2 $OUT/smoke.log ;;
+    bench)
+      timeout -k 10 500 python bench.py $BA > $OUT/bench.json 2> $OUT/bench.err || fail bench $OUT/bench.err
+      cat $OUT/bench.json ;;
+    bench2)
+      timeout -k 10 500 python bench.py --config 2 --no-cpu-baseline $BA > $OUT/bench_cfg2.json 2> $OUT/bench_cfg2.err || fail bench2 $OUT/bench_cfg2.err
+      cat $OUT/bench_cfg2.json ;;
+    rows125k)
+      timeout -k 10 300 python bench.py --rows 125000 --profile-only --steps 200 --warmup 50 $BA > $OUT/rows125k.json 2> $OUT/rows125k.err || fail rows125k $OUT/rows125k.err
+      cat $OUT/rows125k.json ;;
+    nq1)
+      for c in 3 2; do
+        timeout -k 10 300 python bench.py --config $c --nq 1 --profile-only --steps 300 --warmup 100 $BA > $OUT/nq1_cfg$c.json 2> $OUT/nq1_cfg$c.err || fail nq1 $OUT/nq1_cfg$c.err
+        cat $OUT/nq1_cfg$c.json
+      done ;;
+    rocprof)
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline $BA > $OUT/prof.log 2>&1 || fail rocprof $OUT/prof.log
+      head -8 $OUT/prof/run_kernel_stats.csv | cut -c1-220 ;;
+    rehearse)
+      n=${arg:-8}
+      IMGREC_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+        --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus $n --steps 3 --warmup 1 --single-query-steps 3 $BA \
+        > $OUT/rehearse_n$n.json 2> $OUT/rehearse_n$n.err || fail rehearse $OUT/rehearse_n$n.err
+      cat $OUT/rehearse_n$n.json ;;
+    pmc)
+      arg=${arg//,/ }                       # pmc=--config,2 -> "--config 2"
+      BENCH_ARGS="$arg" bash tools/pmc_clock.sh $TAG/pmcclk > $OUT/pmc_clock.log 2>&1 || fail pmc $OUT/pmc_clock.log
+      cat $OUT/pmc_clock.log
+      BENCH_ARGS="$arg" bash tools/pmc_traffic.sh $TAG > $OUT/pmc_traffic.log 2>&1 || fail pmc $OUT/pmc_traffic.log
+      tail -12 $OUT/pmc_traffic.log ;;
+    stamps)
+      IMGREC_STAMPS_CFG=${arg:-3} IMGREC_STAMPS_FN=knn_b16w_stamps_read timeout -k 10 300 python tools/b16_stamps.py \
+        > $OUT/stamps_cfg${arg:-3}.json 2> $OUT/stamps_cfg${arg:-3}.err || fail stamps $OUT/stamps_cfg${arg:-3}.err
+      cat $OUT/stamps_cfg${arg:-3}.err ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-pmcclk}; mkdir -p $OUT
 R="--kernel-trace --kernel-include-regex knn_b16 --output-format csv"
 for v in ${LIBS:-libimgrec.so}; do
-  IMGREC_LIB_NAME=$v timeout -s KILL 120 rocprofv3 $R --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA -d $OUT/$v -o run -- python3 bench.py --profile-only --steps 3 --warmup 1 > $OUT/$v.log 2>&1 || { echo "$v failed"; tail -5 $OUT/$v.log; exit 2; }
+  IMGREC_LIB_NAME=$v timeout -s KILL 120 rocprofv3 $R --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA -d $OUT/$v -o run -- python3 bench.py --profile-only --steps 3 --warmup 1 ${BENCH_ARGS:-} > $OUT/$v.log 2>&1 || { echo "$v failed"; tail -5 $OUT/$v.log; exit 2; }
   python3 - $OUT/$v <<'PY'
 import collections, csv, glob, sys
 d = sys.argv[1]
