@@ -79,6 +79,7 @@ SIGNATURES = {
     "vit_patchify_bf16": (_i, [_vp, _i64, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "vit_tokens_f32": (_i, [_vp, _vp, _vp, _i64, _i, _i, _vp, _vp]),
     "vit_attention_bf16": (_i, [_vp, _i64, _i, _i, _i, C.c_float, _vp, _vp]),
+    "vit_linear_bf16": (_i, [_vp, _vp, _vp, _i64, _i, _i, _i, _vp, _vp]),
     "color_hist_batch_async": (_i, [_vp, _i64, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp]),
     # imgrec_ingest.h
     "ingest_parse_f32": (_i64, [_vp, _i64, _vp, _i64]),

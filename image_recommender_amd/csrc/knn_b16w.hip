@@ -32,6 +32,7 @@
 #include <type_traits>
 
 #include "knn_kernels.h"
+#include "lds_dma.h"
 
 namespace imgrec {
 namespace {
@@ -72,51 +73,6 @@ static_assert(kBKW == 32 && kCPR == 8, "stage depth: two 32-deep k-steps per sta
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
 static_assert(kDeferQ >= 0 && kDeferQ < kQuads - 1, "deferred DMA inside the stage's first quads");
-
-__device__ __forceinline__ uint32_t lds_u32(const void* p) {
-    return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-}
-
-// Four one-KiB LDS-DMA pieces under one M0 value (instruction offsets move both the global source
-// and the LDS destination; the per-lane offsets are pre-reduced by j KiB).
-__device__ __forceinline__ void dma4x(const void* sbase, uint32_t lds0, uint32_t v0, uint32_t v1,
-                                      uint32_t v2, uint32_t v3) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %5\n\t"
-        "global_load_lds_dwordx4 %2, %5 offset:1024\n\t"
-        "global_load_lds_dwordx4 %3, %5 offset:2048\n\t"
-        "global_load_lds_dwordx4 %4, %5 offset:3072\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds0))
-        : "memory");
-}
-
-template <int OFF>
-__device__ __forceinline__ void dma1(const void* sbase, uint32_t lds0, uint32_t v) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, %2 offset:%4\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(v), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds0)), "n"(OFF)
-        : "memory");
-}
-
-__device__ __forceinline__ void dma4_norm(const float* g, uint32_t lds) {
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
-}
-
-__device__ __forceinline__ void barrier_lds() {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
 
 // Ascending register list, labels arriving in increasing order per lane: slot p's key is the
 // median of (kd[p-1], d, kd[p]); selects stay v_cndmask (no branches); d = +inf is a no-op.

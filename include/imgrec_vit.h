@@ -51,6 +51,20 @@ int vit_tokens_f32(const uint16_t* patch_emb, const float* cls, const float* pos
 int vit_attention_bf16(const uint16_t* qkv, int64_t batch, int ntok, int heads, int head_dim,
                        float scale, uint16_t* out, void* stream);
 
+/* Activation of vit_linear_bf16's epilogue, applied in fp32 before the bf16 rounding. */
+enum vit_act {
+    VIT_ACT_NONE = 0,
+    VIT_ACT_GELU_ERF = 1,    /* nn.GELU: 0.5 x (1 + erf(x / sqrt 2)) (DINO, OpenCLIP MLPs) */
+    VIT_ACT_GELU_TANH = 2,   /* nn.GELU(approximate="tanh") */
+    VIT_ACT_QUICK_GELU = 3   /* CLIP's QuickGELU: x sigmoid(1.702 x) */
+};
+
+/* y (m x n) = bf16(act(x w^T + bias)): x (m x k) and w (n x k, nn.Linear's weight layout) bf16
+ * row-major, bias fp32 (n) or NULL, fp32 accumulation (F.linear's product, csrc/vit_gemm.hip).
+ * k a multiple of 64, n a multiple of 256, 16-B aligned pointers; any m. */
+int vit_linear_bf16(const uint16_t* x, const uint16_t* w, const float* bias, int64_t m, int k,
+                    int n, int act, uint16_t* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

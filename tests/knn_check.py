@@ -109,9 +109,10 @@ def check_knn_tight(D, I, xb, xq, k, metric="l2", oracle=None, blas=None, min_ra
     worst_rel = 0.0
     for q in range(nq):
         gd = Dg[q]
-        scale = float(np.abs(gd[:nv + 1][Ig[q, :nv + 1] >= 0]).max()) + 1e-30
+        scale = float(np.abs(gd[:nv + 1][Ig[q, :nv + 1] >= 0]).max())
         w = max(WINDOW_MULT * E, WINDOW_REL_FLOOR * scale)
-        worst_rel = max(worst_rel, w / scale)
+        if scale > 0:                      # (a query whose answers all sit at distance 0: no scale)
+            worst_rel = max(worst_rel, w / scale)
         for j in range(nv):
             rank_tot += 1
             lo = j == 0 or abs(gd[j] - gd[j - 1]) > w
