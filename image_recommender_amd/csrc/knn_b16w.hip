@@ -339,6 +339,7 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
 #ifdef IMGREC_B16_STAMPS
         const bool stamp_on = blockIdx.x == 100 && t - t0 < 120;
         int nit = 0;
+        unsigned long long ins_cyc = 0;      // cycles inside the insertion blocks of this tile
 #endif
         f32x4 acc[kRB][2];
 #pragma unroll
@@ -458,6 +459,9 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                     msk[h] = __builtin_amdgcn_alignbit(msk[h], __float_as_uint(dlo.x), 31);
                 }
             }
+#ifdef IMGREC_B16_STAMPS
+            const unsigned long long ins0 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const unsigned m = msk[h] & live;
@@ -496,6 +500,9 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                     }
                 }
             }
+#ifdef IMGREC_B16_STAMPS
+            ins_cyc += __builtin_amdgcn_s_memtime() - ins0;
+#endif
         }
         B16W_STAMP(2 * (t - t0) + 1);
         // sibling lockstep (TileArgs::sync): publish this tile, wait (bounded) until the G
@@ -523,6 +530,7 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
         }
 #ifdef IMGREC_B16_STAMPS
         if (stamp_on && lane == 0) g_b16w_stamps[wave * 256 + 128 + (t - t0)] = (unsigned long long)nit;
+        if (stamp_on && lane == 0 && t - t0 < 64) g_b16w_stamps[wave * 256 + 192 + (t - t0)] = ins_cyc;
 #endif
         if (g < total) {
             read_a(smem + (g & 1) * kStage, 0, fa[0]);

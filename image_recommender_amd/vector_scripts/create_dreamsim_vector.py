@@ -110,6 +110,36 @@ def _lin_gelu(m, x):
     return y.view(*shp[:-1], y.shape[-1])
 
 
+_ACT = {"none": 0, "gelu": 1, "gelu_tanh": 2, "quick_gelu": 3}     # include/imgrec_vit.h vit_act
+
+
+def _hlin(m, x, act="none"):
+    """act(x W^T + b) of a prepared Linear / patch projection in ONE HIP kernel
+    (include/imgrec_vit.h vit_linear_bf16, csrc/vit_gemm.hip): bf16 operands, fp32 accumulation,
+    the fp32 bias and the activation (nn.GELU's erf form, CLIP's QuickGELU) applied before the
+    bf16 rounding of the output.  Shapes the kernel does not take (k % 64, n % 256) go through
+    _lin (and the activation as a separate pass)."""
+    import ctypes as C
+
+    import torch
+    from .. import _lib
+    w = m.w_lp
+    n, k = w.shape
+    if k % 64 or n % 256 or x.dtype != torch.bfloat16:
+        y = _lin(m, x)
+        return {"none": lambda t: t, "gelu": _gelu_, "quick_gelu": _quick_gelu_}[act](y.contiguous())
+    x = x.contiguous()
+    y = torch.empty((*x.shape[:-1], n), dtype=torch.bfloat16, device=x.device)
+    b = getattr(m, "b_f32", None)
+    rc = _lib.load().vit_linear_bf16(C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()),
+                                     C.c_void_p(b.data_ptr() if b is not None else None),
+                                     x.numel() // k, k, n, _ACT[act], C.c_void_p(y.data_ptr()),
+                                     C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    if rc != 0:
+        raise RuntimeError("vit_linear_bf16 failed")
+    return y
+
+
 def _patchify(img, mean, std, p):
     """(B, 3, H, W) fp32 image -> bf16 GEMM rows (B, (H/p)(W/p), 3 p p) of ((img - mean) / std),
     patches laid out (c, kh, kw) — one HIP pass (vit_patchify_bf16) for the normalisation, the
@@ -228,6 +258,16 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             """The same block on the fused kernels: x (fp32 residual, updated in place) first takes
             the previous block's bf16 output `delta`; returns this block's bf16 output."""
             b, n, c = x.shape
+            if getattr(self, "hip_gemm", False):
+                # every matrix product (and fc1's activation) on vit_linear_bf16
+                qkv = _hlin(self.qkv, _add_ln(x, delta, self.ln1))
+                a = _attn(qkv, self.heads) if getattr(self, "hip_attn", False) else \
+                    F.scaled_dot_product_attention(
+                        *qkv.view(b, n, 3, self.heads, c // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
+                    ).transpose(1, 2).reshape(b, n, c)
+                y = _add_ln(x, _hlin(self.proj, a), self.ln2)
+                h = _hlin(self.fc1, y, "quick_gelu" if self.quick_gelu else "gelu")
+                return _hlin(self.fc2, h)
             qkv = _lin(self.qkv, _add_ln(x, delta, self.ln1))
             if getattr(self, "hip_attn", False):
                 a = _attn(qkv, self.heads)
@@ -267,7 +307,8 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             if getattr(self, "fused", False) and w is not None:
                 # normalisation + patch extraction, the patch GEMM, then cls / pos in one pass
                 p = self.patch.kernel_size[0]
-                t = F.linear(_patchify(x, self.mean, self.std, p), w, self.patch.b_lp)
+                pt = _patchify(x, self.mean, self.std, p)
+                t = _hlin(self.patch, pt) if getattr(self, "hip_gemm", False) else F.linear(pt, w, self.patch.b_lp)
                 x = self.ln_pre(_tokens(t, self.cls, self.pos))
                 delta = None
                 for blk in self.blocks:
@@ -308,24 +349,30 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             parts = [F.normalize(t(x).float(), dim=-1) for t in self.towers]
             return torch.cat(parts, -1)
 
-        def prepare_inference(self, dtype, fused=False, gelu_epilogue=False, hip_attn=None):
+        def prepare_inference(self, dtype, fused=False, gelu_epilogue=False, hip_attn=None,
+                              hip_gemm=None):
             """Cache low-precision copies of every matrix-product weight once (autocast would
             re-cast them on every forward); LayerNorms and the residual stream stay fp32.
             fused (bf16, on a GPU): residual add + LayerNorm + bf16 cast and QuickGELU run as
-            single HIP passes (include/imgrec_vit.h).  gelu_epilogue (with fused): the erf
-            GELU after fc1 becomes the GEMM's own epilogue (_lin_gelu).  hip_attn (with fused;
-            default on): attention through the one-kernel vit_attention_bf16 (_attn) instead of
-            torch SDPA."""
+            single HIP passes (include/imgrec_vit.h).  gelu_epilogue (with fused, without
+            hip_gemm): the GELU after fc1 as hipBLASLt's GELU_BIAS epilogue (_lin_gelu).
+            hip_attn (with fused; default on): attention through the one-kernel
+            vit_attention_bf16 (_attn) instead of torch SDPA.  hip_gemm (with fused; default
+            on): every matrix product, with its bias and fc1's activation (erf GELU / QuickGELU),
+            on the HIP GEMM vit_linear_bf16 (_hlin) instead of hipBLASLt."""
             for t in self.towers:
                 t.fused = bool(fused) and dtype == torch.bfloat16
+                t.hip_gemm = t.fused and (hip_gemm is None or bool(hip_gemm))
                 for blk in t.blocks:
                     blk.gelu_epilogue = t.fused and bool(gelu_epilogue)
                     blk.hip_attn = t.fused and (hip_attn is None or bool(hip_attn))
+                    blk.hip_gemm = t.hip_gemm
             for m in self.modules():
                 if isinstance(m, (nn.Linear, nn.Conv2d)):
                     w = m.weight.detach()
                     m.w_lp = (w.reshape(w.shape[0], -1) if w.dim() > 2 else w).to(dtype).contiguous()
                     m.b_lp = m.bias.detach().to(dtype) if m.bias is not None else None
+                    m.b_f32 = m.bias.detach().float().contiguous() if m.bias is not None else None
             return self
 
     if seed is not None:

@@ -1,0 +1,99 @@
+"""vit_linear_bf16 (include/imgrec_vit.h, csrc/vit_gemm.hip) — the HIP GEMM behind every matrix
+product of the DreamSim-architecture forward — against a plain PyTorch fp32 reference of the same
+op, act(x W^T + b) on the same bf16 operands, and the forward built on it against the hipBLASLt
+one (/root/reference/vector_scripts/create_dreamsim_vector.py:51-93 embeds with this
+architecture; its values are parity-unpinned: no pretrained weights here).
+
+Tolerance, stated: the output is one bf16 rounding of an fp32 sum, so |y - ref| <= 2^-8 |ref|
+(round to nearest: half an ulp of 2^-7 relative) + 2^-20 sum_i |x_i w_i| (fp32 accumulation-order
+slack of a K <= 3072 dot product; the rigorous gamma_K is ~2e-4 of that sum, the observed ~1e-6)
++ the activation's own fp32 evaluation (erff / __expf: a few ulps, inside the first term).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ACTS = {"none": lambda t: t, "gelu": lambda t: torch.nn.functional.gelu(t),
+        "quick_gelu": lambda t: t * torch.sigmoid(1.702 * t),
+        "gelu_tanh": lambda t: torch.nn.functional.gelu(t, approximate="tanh")}
+
+
+def _linear(m, k, n, act="none", bias=True, seed=0, scale=1.0):
+    from types import SimpleNamespace
+
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import _hlin
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = (torch.randn(m, k, device="cuda", generator=g) * scale).bfloat16()
+    w = (torch.randn(n, k, device="cuda", generator=g) / k ** 0.5).bfloat16()
+    b = torch.randn(n, device="cuda", generator=g) if bias else None
+    mod = SimpleNamespace(w_lp=w.contiguous(), b_lp=b.bfloat16() if bias else None,
+                          b_f32=b.contiguous() if bias else None)
+    y = _hlin(mod, x, act)
+    torch.cuda.synchronize()
+    ref = x.float() @ w.float().T + (b if bias else 0.0)
+    ref = ACTS[act](ref)
+    absum = x.float().abs() @ w.float().abs().T
+    return y, ref, absum
+
+
+def _within(y, ref, absum):
+    err = (y.float() - ref).abs()
+    bound = ref.abs() * 2.0 ** -8 + absum * 2.0 ** -20 + 1e-30
+    worst = float((err / bound).max())
+    assert worst <= 1.0, worst
+    return worst
+
+
+@pytest.mark.parametrize("m,k,n", [(197 * 2, 768, 2304), (197, 768, 768), (512, 768, 3072),
+                                   (394, 3072, 768), (1, 768, 256), (7, 64, 256), (8 * 197, 768, 768),
+                                   (5000, 128, 512), (256 * 3 + 1, 256, 512)])
+def test_linear_matches_fp32_reference(gpu, m, k, n):
+    """Shapes of the forward (qkv / proj / fc1 / fc2 at 1-8 images), a single row, tails of a
+    256-row tile (m = 197, 769: rows past M staged from row M - 1 and never stored), more token
+    tiles than splits (m = 5000)."""
+    y, ref, absum = _linear(m, k, n, seed=m + k + n)
+    assert y.shape == (m, n) and y.dtype == torch.bfloat16
+    _within(y, ref, absum)
+
+
+@pytest.mark.parametrize("act", ["gelu", "quick_gelu", "gelu_tanh"])
+def test_linear_activation_epilogue(gpu, act):
+    """fc1's activation in the epilogue (fp32, before the bf16 rounding): nn.GELU's erf form
+    (DINO / OpenCLIP), CLIP's QuickGELU, the tanh form."""
+    y, ref, absum = _linear(197 * 3, 768, 3072, act, seed=7, scale=2.0)
+    _within(y, ref, absum)
+
+
+def test_linear_without_bias_and_refusals(gpu):
+    """No bias (the CLIP / OpenCLIP patch projections); shapes the kernel does not take are
+    refused by the C ABI (k % 64, n % 256, misaligned) and served by _lin in _hlin."""
+    import ctypes as C
+
+    from image_recommender_amd import _lib
+    y, ref, absum = _linear(300, 768, 768, bias=False, seed=3)
+    _within(y, ref, absum)
+    lib = _lib.load()
+    x = torch.zeros(10, 96, dtype=torch.bfloat16, device="cuda")
+    w = torch.zeros(256, 96, dtype=torch.bfloat16, device="cuda")
+    out = torch.empty(10, 256, dtype=torch.bfloat16, device="cuda")
+    assert lib.vit_linear_bf16(C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()), None, 10, 96,
+                               256, 0, C.c_void_p(out.data_ptr()), None) == -1
+    y2, ref2, absum2 = _linear(10, 96, 200, seed=4)              # k % 64 and n % 256: _lin path
+    _within(y2, ref2, absum2)
+
+
+def test_forward_on_hip_gemm_matches_hipblaslt(gpu):
+    """The fused forward with every GEMM on vit_linear_bf16 against the same forward on
+    hipBLASLt (same weights, 6 images, 4 blocks per tower): cosine > 0.999 per image."""
+    from image_recommender_amd.vector_scripts.create_dreamsim_vector import build_ensemble
+    x = torch.rand((6, 3, 224, 224), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    lt = build_ensemble(seed=0, depth=4).cuda().eval().prepare_inference(torch.bfloat16, fused=True,
+                                                                         hip_gemm=False)
+    hg = build_ensemble(seed=0, depth=4).cuda().eval().prepare_inference(torch.bfloat16, fused=True)
+    assert all(t.hip_gemm for t in hg.towers) and not any(t.hip_gemm for t in lt.towers)
+    with torch.no_grad():
+        a = torch.nn.functional.normalize(lt.embed(x).float(), dim=-1)
+        b = torch.nn.functional.normalize(hg.embed(x).float(), dim=-1)
+    cos = (a * b).sum(-1)
+    assert float(cos.min()) > 0.999, cos

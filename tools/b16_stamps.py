@@ -50,6 +50,10 @@ nit = a[:, 128:128 + ntile]
 print("insert-loop iterations per tile (wave 0): first", nit[0, :4].tolist(), "median", float(np.median(nit[0, 1:])),
       "mean", float(nit[0, 1:].mean()), "(all waves mean", float(nit[:, 1:].mean()), ")", file=sys.stderr)
 out["insert_iterations"] = nit.tolist()
+ins = a[:, 192:192 + min(ntile, 64)]
+out["insert_cycles"] = ins.tolist()
+print("cycles in the insertion blocks per tile: median per wave", [float(np.median(ins[w, 1:])) for w in range(8)],
+      "(epilogue median per wave", [float(np.median(epi[w, 1:])) for w in range(8)], ")", file=sys.stderr)
 tile = np.median(loop[0]) + np.median(epi.max(0)[1:])
 print(f"tile period ~{tile:.0f}; ideal MFMA {nst * 2048}", file=sys.stderr)
 print(json.dumps(out))

@@ -13,6 +13,8 @@ images/s of variants on one GPU, random weights, bf16 autocast, 224 x 224 inputs
   fused_gelu_lt  fused + fc1's GELU as the hipBLASLt GELU_BIAS epilogue (torch._addmm_activation)
              + attention as one HIP kernel (vit_attention_bf16, the default since round 3)
   fused_gelu_lt_sdpa  the same with attention on torch SDPA (round 3's earlier form)
+  hip_gemm   fused + every GEMM (bias, fc1's erf GELU / QuickGELU in the epilogue) on the HIP
+             kernel vit_linear_bf16 instead of hipBLASLt (the default since round 4)
   X@B        variant X with SDPA restricted to backend B (flash / efficient / math)
 
 FLOP per image: 3 ViT-B/16 towers at 224 (197 tokens): 2 x 17.58 GMAC each -> 105.5 GFLOP;
@@ -46,19 +48,20 @@ def main():
     model = build_ensemble(seed=0).to(dev).eval()
     cached = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16)
     fused = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True,
-                                                                   hip_attn=False)
+                                                                   hip_attn=False, hip_gemm=False)
     fused_lt = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True,
-                                                                      gelu_epilogue=True)
+                                                                      gelu_epilogue=True, hip_gemm=False)
     fused_lt_sdpa = build_ensemble(seed=0).to(dev).eval().prepare_inference(
-        torch.bfloat16, fused=True, gelu_epilogue=True, hip_attn=False)
+        torch.bfloat16, fused=True, gelu_epilogue=True, hip_attn=False, hip_gemm=False)
+    hip_gemm = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True)
 
     def embed(x):
         if var_now[0].startswith("autocast"):        # per-call weight casts (the r01 form)
             with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
                 return torch.nn.functional.normalize(model.embed(x).float(), dim=-1)
         with torch.no_grad():                          # weights cast once (the shipped form)
-            m = {"fused": fused, "fused_gelu_lt": fused_lt,
-                 "fused_gelu_lt_sdpa": fused_lt_sdpa}.get(var_now[0].split("@")[0], cached)
+            m = {"fused": fused, "fused_gelu_lt": fused_lt, "fused_gelu_lt_sdpa": fused_lt_sdpa,
+                 "hip_gemm": hip_gemm}.get(var_now[0].split("@")[0], cached)
             return torch.nn.functional.normalize(m.embed(x).float(), dim=-1)
 
     var_now = [""]

@@ -13,6 +13,9 @@
 #   rehearse=N      gloo N-rank rehearsal of bench.py on this one GPU -> rehearse_nN.json
 #   pmc[=ARGS]      clock/MFMA-busy and HBM-traffic passes of the candidate kernel (bench args,
 #                   comma-separated: pmc=--config,2)
+#   vit             vit_gemm_rate.py (the forward's GEMM shapes, HIP vs hipBLASLt) + dreamsim_variants.py
+#                   at batch 512 (hipBLASLt forward vs HIP-GEMM forward) -> vit_gemm_rate.jsonl, ds_variants.jsonl
+#   probe=CFG       tools/i8_cfg2_probe.py: 32 single queries, certificate counts and times -> probe_cfgN.jsonl
 #   stamps=CFG      per-tile stage-loop / epilogue cycles of the 256 x 256 bf16 kernel on bench
 #                   config CFG (lib/libimgrec_stamps.so: tools/build_variants.sh stamps -DIMGREC_B16_STAMPS)
 # Extra bench arguments for every bench stage: BENCH_ARGS.
@@ -64,6 +67,15 @@ for st in "$@"; do
       cat $OUT/pmc_clock.log
       BENCH_ARGS="$arg" bash tools/pmc_traffic.sh $TAG > $OUT/pmc_traffic.log 2>&1 || fail pmc $OUT/pmc_traffic.log
       tail -12 $OUT/pmc_traffic.log ;;
+    vit)
+      timeout -k 10 300 python tools/vit_gemm_rate.py > $OUT/vit_gemm_rate.jsonl 2> $OUT/vit_gemm_rate.err || fail vit $OUT/vit_gemm_rate.err
+      cat $OUT/vit_gemm_rate.jsonl
+      timeout -k 10 400 python tools/dreamsim_variants.py --batches 512 --iters 6 --variants fused_gelu_lt,hip_gemm,fused_gelu_lt,hip_gemm \
+        > $OUT/ds_variants.jsonl 2> $OUT/ds_variants.err || fail vit $OUT/ds_variants.err
+      cat $OUT/ds_variants.jsonl ;;
+    probe)
+      CFG=${arg:-2} timeout -k 10 300 python tools/i8_cfg2_probe.py > $OUT/probe_cfg${arg:-2}.jsonl 2> $OUT/probe_cfg${arg:-2}.err || fail probe $OUT/probe_cfg${arg:-2}.err
+      cat $OUT/probe_cfg${arg:-2}.jsonl ;;
     stamps)
       IMGREC_STAMPS_CFG=${arg:-3} IMGREC_STAMPS_FN=knn_b16w_stamps_read timeout -k 10 300 python tools/b16_stamps.py \
         > $OUT/stamps_cfg${arg:-3}.json 2> $OUT/stamps_cfg${arg:-3}.err || fail stamps $OUT/stamps_cfg${arg:-3}.err
