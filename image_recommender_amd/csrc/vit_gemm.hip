@@ -21,8 +21,9 @@
 //   0-3 move the token tile, 4-7 the weight tile (their issue deferred into the next stage);
 // * the MFMA takes the WEIGHT fragment as its A operand and the token fragment as B, so a lane's
 //   accumulator holds four consecutive output features of one token (row = 4 (lane >> 4) + reg,
-//   col = lane & 15): the epilogue adds the bias, applies the activation in fp32, rounds to bf16
-//   and stores 8 contiguous bytes per (token, feature quad) — 32 stores per lane per tile;
+//   col = lane & 15): the epilogue adds the bias, applies the activation in fp32, rounds to bf16,
+//   pairs lane quarters by v_permlane16_swap and stores 16 contiguous bytes per (token, 8
+//   features) — 16 stores per lane per tile;
 // * 8 waves along the features (32 each) x all 256 tokens of the tile: 16 token blocks x 2
 //   feature blocks of 16 x 16, 128 accumulator registers per lane.
 // Requirements (checked by the launcher): K a multiple of 64, N a multiple of 256, 16-B aligned
@@ -266,21 +267,33 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
         else if (nlive == 2) stage_loop(std::integral_constant<int, 2>{});
         else stage_loop(std::integral_constant<int, 1>{});
 
-        // ---- epilogue: bias, activation, bf16, one 8-B store per (token, feature quad)
+        // ---- epilogue: bias, activation, bf16; then one 16-B store per (token, 8 features): a
+        // lane holds features 4 lq .. + 3 of both feature blocks h = 0, 1 (16 apart), and a
+        // v_permlane16_swap per dword pairs lane quarters lq, lq + 1 (cdna_hip_programming.md T21,
+        // the 16-lane form): even quarters end with h = 0's features 4 lq .. 4 lq + 7, odd ones with
+        // h = 1's 16 + 4 (lq - 1) .. + 7 — half the store instructions of 8-B stores, whose issue
+        // rate, not HBM, sets this tail
 #pragma unroll
         for (int rb = 0; rb < kRB; ++rb) {
             const int tok = row0 + 16 * rb + lc;
-            uint16_t* yrow = y + (size_t)tok * N + fcol;
+            uint32_t o[2][2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const f32x4 v = acc[rb][h] + bv[h];
                 const f32x2 lo = (f32x2){activate<ACT>(v[0]), activate<ACT>(v[1])};
                 const f32x2 hi = (f32x2){activate<ACT>(v[2]), activate<ACT>(v[3])};
-                const bf16x2 blo = __builtin_convertvector(lo, bf16x2);
-                const bf16x2 bhi = __builtin_convertvector(hi, bf16x2);
-                const uint2 o = make_uint2(__builtin_bit_cast(uint32_t, blo), __builtin_bit_cast(uint32_t, bhi));
-                if (tok < M) *reinterpret_cast<uint2*>(yrow + 16 * h) = o;
+                o[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(lo, bf16x2));
+                o[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hi, bf16x2));
             }
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+                const auto r = __builtin_amdgcn_permlane16_swap(o[0][d], o[1][d], false, false);
+                o[0][d] = r[0];
+                o[1][d] = r[1];
+            }
+            if (tok < M)
+                *reinterpret_cast<uint4*>(y + (size_t)tok * N + fcol + ((lq & 1) ? 12 : 0)) =
+                    make_uint4(o[0][0], o[0][1], o[1][0], o[1][1]);
         }
         if (g < total) {
             read_a(smem + (g & 1) * kStage, 0, fa[0]);

@@ -266,7 +266,10 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
                         *qkv.view(b, n, 3, self.heads, c // self.heads).permute(2, 0, 3, 1, 4).unbind(0)
                     ).transpose(1, 2).reshape(b, n, c)
                 y = _add_ln(x, _hlin(self.proj, a), self.ln2)
-                h = _hlin(self.fc1, y, "quick_gelu" if self.quick_gelu else "gelu")
+                # (gelu_epilogue: the tanh form, as hipBLASLt's GELU_BIAS epilogue computes it —
+                # within the bf16 rounding of the erf form, test_gelu_epilogue_within_bf16_of_erf_gelu)
+                h = _hlin(self.fc1, y, "quick_gelu" if self.quick_gelu else
+                          ("gelu_tanh" if getattr(self, "gelu_epilogue", False) else "gelu"))
                 return _hlin(self.fc2, h)
             qkv = _lin(self.qkv, _add_ln(x, delta, self.ln1))
             if getattr(self, "hip_attn", False):
@@ -358,8 +361,9 @@ def build_ensemble(seed: int | None = 0, depth: int = 12):
             hip_gemm): the GELU after fc1 as hipBLASLt's GELU_BIAS epilogue (_lin_gelu).
             hip_attn (with fused; default on): attention through the one-kernel
             vit_attention_bf16 (_attn) instead of torch SDPA.  hip_gemm (with fused; default
-            on): every matrix product, with its bias and fc1's activation (erf GELU / QuickGELU),
-            on the HIP GEMM vit_linear_bf16 (_hlin) instead of hipBLASLt."""
+            on): every matrix product, with its bias and fc1's activation (QuickGELU; GELU in
+            the erf form, or the tanh form with gelu_epilogue), on the HIP GEMM vit_linear_bf16
+            (_hlin) instead of hipBLASLt."""
             for t in self.towers:
                 t.fused = bool(fused) and dtype == torch.bfloat16
                 t.hip_gemm = t.fused and (hip_gemm is None or bool(hip_gemm))

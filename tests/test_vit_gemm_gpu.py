@@ -19,7 +19,9 @@ ACTS = {"none": lambda t: t, "gelu": lambda t: torch.nn.functional.gelu(t),
         "gelu_tanh": lambda t: torch.nn.functional.gelu(t, approximate="tanh")}
 
 
-def _linear(m, k, n, act="none", bias=True, seed=0, scale=1.0):
+def _linear(m, k, n, act="none", bias=True, seed=0, scale=1.0, bf16_bias=False):
+    """(y, fp32 reference, sum |x_i w_i|); bf16_bias: the reference adds the bias rounded to bf16
+    (what _lin's F.linear fallback adds)."""
     from types import SimpleNamespace
 
     from image_recommender_amd.vector_scripts.create_dreamsim_vector import _hlin
@@ -31,7 +33,7 @@ def _linear(m, k, n, act="none", bias=True, seed=0, scale=1.0):
                           b_f32=b.contiguous() if bias else None)
     y = _hlin(mod, x, act)
     torch.cuda.synchronize()
-    ref = x.float() @ w.float().T + (b if bias else 0.0)
+    ref = x.float() @ w.float().T + ((b.bfloat16().float() if bf16_bias else b) if bias else 0.0)
     ref = ACTS[act](ref)
     absum = x.float().abs() @ w.float().abs().T
     return y, ref, absum
@@ -79,7 +81,7 @@ def test_linear_without_bias_and_refusals(gpu):
     out = torch.empty(10, 256, dtype=torch.bfloat16, device="cuda")
     assert lib.vit_linear_bf16(C.c_void_p(x.data_ptr()), C.c_void_p(w.data_ptr()), None, 10, 96,
                                256, 0, C.c_void_p(out.data_ptr()), None) == -1
-    y2, ref2, absum2 = _linear(10, 96, 200, seed=4)              # k % 64 and n % 256: _lin path
+    y2, ref2, absum2 = _linear(10, 96, 200, seed=4, bf16_bias=True)   # k % 64, n % 256: _lin path
     _within(y2, ref2, absum2)
 
 

@@ -16,8 +16,11 @@
 #   vit             vit_gemm_rate.py (the forward's GEMM shapes, HIP vs hipBLASLt) + dreamsim_variants.py
 #                   at batch 512 (hipBLASLt forward vs HIP-GEMM forward) -> vit_gemm_rate.jsonl, ds_variants.jsonl
 #   probe=CFG       tools/i8_cfg2_probe.py: 32 single queries, certificate counts and times -> probe_cfgN.jsonl
-#   stamps=CFG      per-tile stage-loop / epilogue cycles of the 256 x 256 bf16 kernel on bench
-#                   config CFG (lib/libimgrec_stamps.so: tools/build_variants.sh stamps -DIMGREC_B16_STAMPS)
+#   stamps=CFG[:LIB] per-tile stage-loop / epilogue cycles of the 256 x 256 bf16 kernel on bench
+#                   config CFG (lib/LIB, default libimgrec_stamps.so: tools/build_variants.sh stamps
+#                   -DIMGREC_B16_STAMPS)
+#   ab=LIB          A/B of lib/libimgrec.so and lib/LIB: per-step and kernel ms on cfg2 and cfg3
+#                   (profile-only, twice alternating) -> ab_LIB.txt
 # Extra bench arguments for every bench stage: BENCH_ARGS.
 set -u
 export PYTHONPATH=$GRAFT_REPO_ROOT
@@ -77,9 +80,20 @@ for st in "$@"; do
       CFG=${arg:-2} timeout -k 10 300 python tools/i8_cfg2_probe.py > $OUT/probe_cfg${arg:-2}.jsonl 2> $OUT/probe_cfg${arg:-2}.err || fail probe $OUT/probe_cfg${arg:-2}.err
       cat $OUT/probe_cfg${arg:-2}.jsonl ;;
     stamps)
-      IMGREC_STAMPS_CFG=${arg:-3} IMGREC_STAMPS_FN=knn_b16w_stamps_read timeout -k 10 300 python tools/b16_stamps.py \
-        > $OUT/stamps_cfg${arg:-3}.json 2> $OUT/stamps_cfg${arg:-3}.err || fail stamps $OUT/stamps_cfg${arg:-3}.err
-      cat $OUT/stamps_cfg${arg:-3}.err ;;
+      c=${arg%%:*}; c=${c:-3}; lib=libimgrec_stamps.so; [ "${arg#*:}" != "$arg" ] && lib=${arg#*:}
+      IMGREC_LIB_NAME=$lib IMGREC_STAMPS_CFG=$c IMGREC_STAMPS_FN=knn_b16w_stamps_read timeout -k 10 300 python tools/b16_stamps.py \
+        > $OUT/stamps_cfg${c}_$lib.json 2> $OUT/stamps_cfg${c}_$lib.err || fail stamps $OUT/stamps_cfg${c}_$lib.err
+      cat $OUT/stamps_cfg${c}_$lib.err ;;
+    ab)
+      for rep in 1 2; do
+        for lib in libimgrec.so $arg; do
+          for c in 2 3; do
+            IMGREC_LIB_NAME=$lib timeout -k 10 200 python bench.py --config $c --profile-only --steps 60 --warmup 20 \
+              > $OUT/ab.json 2>> $OUT/ab.err || fail ab $OUT/ab.err
+            python3 -c "import json;d=json.load(open('$OUT/ab.json'));print('$rep $lib cfg$c step', round(d['ms_per_step'],4), 'kernel', round(d['kernel_ms'],4))" | tee -a $OUT/ab_$arg.txt
+          done
+        done
+      done ;;
     *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
