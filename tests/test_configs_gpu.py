@@ -270,6 +270,39 @@ def test_cfg5_pipeline_smoke(gpu):
         np.testing.assert_array_equal(got[i], color_counts(host[i], 16))
 
 
+def test_cfg5_pipeline_full_size_one_gpu(gpu):
+    """BASELINE.json configs[4] at its stated 100,000 images (on one GPU; the 8-GPU form is the
+    driver's scaling run): the HIP colour histogram, the DreamSim-architecture forward (every GEMM
+    on vit_linear_bf16), the index add and 1024 searches; every query image finds itself at rank 0
+    and the colour counts of images spread over the whole range equal the integer oracle's
+    (/root/reference/vector_scripts/create_color_vector.py:18-52, create_dreamsim_vector.py:51-93)."""
+    import ctypes as C
+    import torch
+    import bench_pipeline as bp
+    from image_recommender_amd import _lib
+    from oracle.color_hist import color_counts
+    out = bp.run(bp.parse(["--images", "100000", "--model-batch", "512", "--nq", "1024",
+                           "--search-reps", "2"]))
+    print(f"cfg5 100k: {out['value']:.0f} images/s, dreamsim {out['stages']['dreamsim']['images_per_s']:.0f}")
+    assert out["config"]["images"] == 100_000
+    assert out["stages"]["search"]["self_match_at_rank0"] == 1.0
+    dev = torch.device("cuda", 0)
+    for g0 in (0, 31_337, 65_535, 99_936):
+        imgs = bp.gen_images(torch, g0, 64, dev)
+        offs = torch.arange(64, dtype=torch.int64, device=dev) * (bp.IMG * bp.IMG * 3)
+        npix = torch.full((64,), bp.IMG * bp.IMG, dtype=torch.int64, device=dev)
+        hist = torch.empty((64, 48), dtype=torch.float32, device=dev)
+        counts = torch.empty((64, 48), dtype=torch.int32, device=dev)
+        assert _lib.load().color_hist_device(C.c_void_p(imgs.data_ptr()), C.c_void_p(offs.data_ptr()),
+                                             C.c_void_p(npix.data_ptr()), 64, 16,
+                                             C.c_void_p(hist.data_ptr()), C.c_void_p(counts.data_ptr()),
+                                             None) == 0
+        torch.cuda.synchronize()
+        host, got = imgs.cpu().numpy(), counts.cpu().numpy()
+        for i in range(0, 64, 9):
+            np.testing.assert_array_equal(got[i], color_counts(host[i], 16))
+
+
 # --------------------------------------------------------------------------------------------
 # cfg2 at its full size (VERDICT r02 item 1)
 # --------------------------------------------------------------------------------------------

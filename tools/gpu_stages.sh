@@ -11,6 +11,8 @@
 #   nq1             bench.py --nq 1 --profile-only, cfg3 and cfg2 -> nq1_cfg{3,2}.json
 #   rocprof         rocprofv3 --kernel-trace --stats of a bench run -> prof/
 #   rehearse=N      gloo N-rank rehearsal of bench.py on this one GPU -> rehearse_nN.json
+#   rehearse_pipe=N gloo N-rank rehearsal of bench_pipeline.py (config 5) on this one GPU -> pipe_nN.json
+#   pipe            bench_pipeline.py, 100k images on this GPU -> pipe.json
 #   pmc[=ARGS]      clock/MFMA-busy and HBM-traffic passes of the candidate kernel (bench args,
 #                   comma-separated: pmc=--config,2)
 #   vit             vit_gemm_rate.py (the forward's GEMM shapes, HIP vs hipBLASLt) + dreamsim_variants.py
@@ -64,6 +66,15 @@ for st in "$@"; do
         --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus $n --steps 3 --warmup 1 --single-query-steps 3 $BA \
         > $OUT/rehearse_n$n.json 2> $OUT/rehearse_n$n.err || fail rehearse $OUT/rehearse_n$n.err
       cat $OUT/rehearse_n$n.json ;;
+    rehearse_pipe)
+      n=${arg:-8}
+      IMGREC_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+        --master-addr 127.0.0.1 --master-port 29534 bench_pipeline.py --gpus $n --images 16384 --model-batch 256 --search-reps 2 \
+        > $OUT/pipe_n$n.json 2> $OUT/pipe_n$n.err || fail rehearse_pipe $OUT/pipe_n$n.err
+      cat $OUT/pipe_n$n.json ;;
+    pipe)
+      timeout -k 10 400 python bench_pipeline.py > $OUT/pipe.json 2> $OUT/pipe.err || fail pipe $OUT/pipe.err
+      cat $OUT/pipe.json ;;
     pmc)
       arg=${arg//,/ }                       # pmc=--config,2 -> "--config 2"
       BENCH_ARGS="$arg" bash tools/pmc_clock.sh $TAG/pmcclk > $OUT/pmc_clock.log 2>&1 || fail pmc $OUT/pmc_clock.log
