@@ -15,6 +15,8 @@ images/s of variants on one GPU, random weights, bf16 autocast, 224 x 224 inputs
   fused_gelu_lt_sdpa  the same with attention on torch SDPA (round 3's earlier form)
   hip_gemm   fused + every GEMM (bias, fc1's erf GELU / QuickGELU in the epilogue) on the HIP
              kernel vit_linear_bf16 instead of hipBLASLt (the default since round 4)
+  hip_gemm_tanh  the same with fc1's GELU in the tanh form (gelu_epilogue: what
+             DreamSimVectorIndexer ships, as hipBLASLt's GELU_BIAS epilogue computes it)
   X@B        variant X with SDPA restricted to backend B (flash / efficient / math)
 
 FLOP per image: 3 ViT-B/16 towers at 224 (197 tokens): 2 x 17.58 GMAC each -> 105.5 GFLOP;
@@ -54,6 +56,8 @@ def main():
     fused_lt_sdpa = build_ensemble(seed=0).to(dev).eval().prepare_inference(
         torch.bfloat16, fused=True, gelu_epilogue=True, hip_attn=False, hip_gemm=False)
     hip_gemm = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True)
+    hip_gemm_tanh = build_ensemble(seed=0).to(dev).eval().prepare_inference(torch.bfloat16, fused=True,
+                                                                           gelu_epilogue=True)
 
     def embed(x):
         if var_now[0].startswith("autocast"):        # per-call weight casts (the r01 form)
@@ -61,7 +65,7 @@ def main():
                 return torch.nn.functional.normalize(model.embed(x).float(), dim=-1)
         with torch.no_grad():                          # weights cast once (the shipped form)
             m = {"fused": fused, "fused_gelu_lt": fused_lt, "fused_gelu_lt_sdpa": fused_lt_sdpa,
-                 "hip_gemm": hip_gemm}.get(var_now[0].split("@")[0], cached)
+                 "hip_gemm": hip_gemm, "hip_gemm_tanh": hip_gemm_tanh}.get(var_now[0].split("@")[0], cached)
             return torch.nn.functional.normalize(m.embed(x).float(), dim=-1)
 
     var_now = [""]

@@ -84,7 +84,7 @@ for st in "$@"; do
     vit)
       timeout -k 10 300 python tools/vit_gemm_rate.py > $OUT/vit_gemm_rate.jsonl 2> $OUT/vit_gemm_rate.err || fail vit $OUT/vit_gemm_rate.err
       cat $OUT/vit_gemm_rate.jsonl
-      timeout -k 10 400 python tools/dreamsim_variants.py --batches 512 --iters 6 --variants fused_gelu_lt,hip_gemm,fused_gelu_lt,hip_gemm \
+      timeout -k 10 400 python tools/dreamsim_variants.py --batches 512 --iters 6 --variants fused_gelu_lt,hip_gemm,hip_gemm_tanh,fused_gelu_lt,hip_gemm,hip_gemm_tanh \
         > $OUT/ds_variants.jsonl 2> $OUT/ds_variants.err || fail vit $OUT/ds_variants.err
       cat $OUT/ds_variants.jsonl ;;
     probe)
