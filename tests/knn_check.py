@@ -42,9 +42,32 @@ def _exact_pair(xb, xq, qi, ids, metric):
     return x @ q
 
 
-def check_knn(D, I, xb, xq, k, metric="l2", min_exact_frac=0.0, oracle=None):
-    """oracle: optional precomputed search_exact(xb, xq, k + 1, metric) (reused by tests that check
-    several searches of one large corpus)."""
+# corpora up to this many (rows x queries) also get the faiss-fp32 restatement in check_knn's
+# empirical-window label check (a numpy sgemm per corpus block: seconds at the largest size)
+BLAS_MAX_WORK = 2_000_000_000
+
+
+def check_knn(D, I, xb, xq, k, metric="l2", min_exact_frac=0.0, oracle=None, tight=True):
+    """The rigorous-window checks (module doc 1-4), then — unless tight=False — the integer-exact
+    label check at the empirical window of check_knn_tight (no minimum fractions: every rank and
+    top-k set separated by more than the window must match the float64 oracle, and for L2 also
+    faiss's fp32 arithmetic restated).  oracle: optional precomputed search_exact(xb, xq, k + 1,
+    metric) (reused by tests that check several searches of one large corpus)."""
+    checked, total = _check_rigorous(D, I, xb, xq, k, metric, min_exact_frac, oracle)
+    if tight:
+        blas = None
+        if metric == "l2" and xb.shape[0] * xq.shape[0] <= BLAS_MAX_WORK and xb.shape[0] >= 1:
+            from oracle.flat_knn import search_blas_fp32_blocked
+            blas = search_blas_fp32_blocked(xb, xq, min(k, xb.shape[0]), threads=8)
+            if blas[1].shape[1] < k:                       # (k > ntotal: only the first nv used)
+                pad = k - blas[1].shape[1]
+                blas = (np.pad(blas[0], ((0, 0), (0, pad)), constant_values=np.inf),
+                        np.pad(blas[1], ((0, 0), (0, pad)), constant_values=-1))
+        _tight_labels(D, I, xb, xq, k, metric, oracle, blas, 0.0, 0.0, "check_knn")
+    return checked, total
+
+
+def _check_rigorous(D, I, xb, xq, k, metric, min_exact_frac, oracle):
     D = np.asarray(D, dtype=np.float64)
     I = np.asarray(I)
     n = xb.shape[0]
@@ -86,12 +109,17 @@ def check_knn(D, I, xb, xq, k, metric="l2", min_exact_frac=0.0, oracle=None):
 
 def check_knn_tight(D, I, xb, xq, k, metric="l2", oracle=None, blas=None, min_rank_frac=0.0,
                     min_set_frac=0.0, tag=""):
-    """check_knn's rigorous checks, then integer-exact labels at the empirical window (module doc).
+    """check_knn's rigorous checks, then integer-exact labels at the empirical window (module doc)
+    held to minimum checked fractions.
 
     oracle: float64 (Dg, Ig) with k + 1 columns (search_exact); blas: the faiss-restated fp32
     result (Db, Ib) of the same queries (search_blas_fp32_blocked), or None.
     Returns {"rank_frac", "set_frac", "err", "window_rel", ...} and prints it."""
-    check_knn(D, I, xb, xq, k, metric, 0.0, oracle)
+    _check_rigorous(D, I, xb, xq, k, metric, 0.0, oracle)
+    return _tight_labels(D, I, xb, xq, k, metric, oracle, blas, min_rank_frac, min_set_frac, tag)
+
+
+def _tight_labels(D, I, xb, xq, k, metric, oracle, blas, min_rank_frac, min_set_frac, tag):
     D = np.asarray(D, dtype=np.float64)
     I = np.asarray(I)
     Dg, Ig = oracle if oracle is not None else search_exact(xb, xq, k + 1, metric)
