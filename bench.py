@@ -69,6 +69,8 @@ def parse():
                     help="search arithmetic (include/imgrec_knn.h knn_search_mode)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only the timed steps (for rocprofv3 runs)")
+    ap.add_argument("--no-phases", action="store_true",
+                    help="skip the per-rank phase region (its event records show in kernel traces)")
     return ap.parse_args()
 
 
@@ -397,7 +399,7 @@ def main():
     split_q, fallback_q, err_ratio = shard.index.search_stats(with_error=True)   # last step
     path = lib.knn_last_path(h)                                # 0 exact, 1 split, 2 bf16, 3 i8
     kel, kern_ms, _ = region(step, a.steps, True)               # candidate-kernel duration
-    per_rank = phases(a.steps)
+    per_rank = None if a.no_phases else phases(a.steps)
     if a.profile_only:
         if rank == 0:
             print(json.dumps({"elapsed_s": elapsed, "ms_per_step": elapsed / a.steps * 1e3,

@@ -17,6 +17,7 @@
 #                   comma-separated: pmc=--config,2)
 #   vit             vit_gemm_rate.py (the forward's GEMM shapes, HIP vs hipBLASLt) + dreamsim_variants.py
 #                   at batch 512 (hipBLASLt forward vs HIP-GEMM forward) -> vit_gemm_rate.jsonl, ds_variants.jsonl
+#   trace=ARGS      kernel timeline of one search step (tools/trace_step.sh, bench args comma-separated)
 #   probe=CFG       tools/i8_cfg2_probe.py: 32 single queries, certificate counts and times -> probe_cfgN.jsonl
 #   stamps=CFG[:LIB] per-tile stage-loop / epilogue cycles of the 256 x 256 bf16 kernel on bench
 #                   config CFG (lib/LIB, default libimgrec_stamps.so: tools/build_variants.sh stamps
@@ -87,6 +88,10 @@ for st in "$@"; do
       timeout -k 10 400 python tools/dreamsim_variants.py --batches 512 --iters 6 --variants fused_gelu_lt,hip_gemm,hip_gemm_tanh,fused_gelu_lt,hip_gemm,hip_gemm_tanh \
         > $OUT/ds_variants.jsonl 2> $OUT/ds_variants.err || fail vit $OUT/ds_variants.err
       cat $OUT/ds_variants.jsonl ;;
+    trace)
+      arg=${arg//,/ }
+      bash tools/trace_step.sh $TAG/trace_$(echo "$arg" | tr ' -' '__') $arg > $OUT/trace.log 2>&1 || fail trace $OUT/trace.log
+      cat $OUT/trace.log ;;
     probe)
       CFG=${arg:-2} timeout -k 10 300 python tools/i8_cfg2_probe.py > $OUT/probe_cfg${arg:-2}.jsonl 2> $OUT/probe_cfg${arg:-2}.err || fail probe $OUT/probe_cfg${arg:-2}.err
       cat $OUT/probe_cfg${arg:-2}.jsonl ;;

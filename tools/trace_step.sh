@@ -5,5 +5,5 @@ set -u
 export PYTHONPATH=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-trace}; shift; mkdir -p $OUT
-timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/t -o run -- python3 bench.py --profile-only "$@" > $OUT/bench.json 2> $OUT/err.log || { tail -5 $OUT/err.log; exit 2; }
+timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $OUT/t -o run -- python3 bench.py --profile-only --no-phases "$@" > $OUT/bench.json 2> $OUT/err.log || { tail -5 $OUT/err.log; exit 2; }
 python3 tools/trace_summary.py $(ls $OUT/t/*/run_kernel_trace.csv $OUT/t/run_kernel_trace.csv 2>/dev/null | head -1) | tee $OUT/timeline.txt
