@@ -172,7 +172,8 @@ __device__ __forceinline__ void grid_barrier(int* ctr, int nwg) {
 // exact (key, label) in the item's workspace and folds its list floor into the item's atomic
 // minimum; the workgroup that completes the item's last slice ranks the S x k survivors (the
 // item's k best are among them), checks the certificate, writes the answer and resets the
-// item's counters.  NW waves per workgroup.
+// item's counters.  NW waves per workgroup.  Returns 0 (not the item's last slice), 1 (the item
+// answered) or 2 (the item queued for the exact re-run).
 struct SecondChanceLDS {
     float w_key[kWideCap], w_apx[kWideCap];
     int64_t w_lab[kWideCap];
@@ -193,14 +194,35 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
 }
 
 template <int NW>
-__device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int item, int slice,
-                                                    SecondChanceLDS& L) {
+__device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item, int slice,
+                                                   SecondChanceLDS& L) {
     constexpr int NT = NW * 64;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc, S = a.sc_slices;
     const int n4 = dp / 4;
     const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
     const int64_t q = a.chance_list[item];
+    const float* rd = a.raw_d + q * a.raw_stride_q;
+    const int64_t* ri = a.raw_i + q * a.raw_stride_q;
+    const int km = a.raw_km;
+    const int nl = (a.raw_lists - slice + S - 1) / S;          // lists slice, slice + S, ...
+    const int ne = nl * km;
+    auto entry = [&](int j) { return (slice + (j / km) * S) * km + j % km; };
+    // the slice's first kPre entries per thread are loaded together with the bounds' inputs (one
+    // dependent round trip instead of two; a one-query second chance is a chain of them)
+    constexpr int kPre = 4;
+    float pv[kPre];
+    int64_t pl[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const int j = t + u * NT;
+        pl[u] = -1;
+        pv[u] = INFINITY;
+        if (j < ne) {
+            pl[u] = ri[entry(j)];
+            pv[u] = rd[entry(j)];
+        }
+    }
     const QueryBounds B(a, q);
     // the same prefix limit as the first pass, from the merged candidates' k-th key
     const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
@@ -211,23 +233,19 @@ __device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int ite
         L.s_ratio = 0u;
     }
     __syncthreads();
-    const float* rd = a.raw_d + q * a.raw_stride_q;
-    const int64_t* ri = a.raw_i + q * a.raw_stride_q;
-    const int km = a.raw_km;
-    const int nl = (a.raw_lists - slice + S - 1) / S;          // lists slice, slice + S, ...
-    for (int j = t; j < nl; j += NT) {
-        const int e = (slice + j * S) * km + km - 1;
-        if (ri[e] >= 0) atomicMin(&L.w_tau, key_bits_ordered(rd[e]));   // a full list: its floor
-    }
-    for (int j = t; j < nl * km; j += NT) {
-        const int e = (slice + (j / km) * S) * km + j % km;
-        const int64_t l = ri[e];
-        const float v = rd[e];
+    // a full list (last entry valid) bounds the rows it dropped: its last key is a floor; the
+    // entries under the prefix limit are reranked
+    auto take = [&](int j, int64_t l, float v) __attribute__((always_inline)) {
+        if (j % km == km - 1 && l >= 0) atomicMin(&L.w_tau, key_bits_ordered(v));
         if (l >= 0 && v <= thr) {
             const int s2 = atomicAdd(&L.w_n, 1);
             if (s2 < kWideCap) { L.w_apx[s2] = v; L.w_lab[s2] = l; }
         }
-    }
+    };
+#pragma unroll
+    for (int u = 0; u < kPre; ++u)
+        if (t + u * NT < ne) take(t + u * NT, pl[u], pv[u]);
+    for (int j = t + kPre * NT; j < ne; j += NT) take(j, ri[entry(j)], rd[entry(j)]);
     __syncthreads();
     const int n = L.w_n;
     const bool overflow = n > kWideCap;
@@ -237,17 +255,18 @@ __device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int ite
         const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
         for (int c0 = wave; c0 < n; c0 += NW * kRerankRows) {
             const float4* r4[kRerankRows];
-            float acc[kRerankRows];
+            float acc[kRerankRows], xr[kRerankRows];
 #pragma unroll
-            for (int v = 0; v < kRerankRows; ++v)
-                r4[v] = reinterpret_cast<const float4*>(
-                    a.xb + (L.w_lab[min(c0 + NW * v, n - 1)] - a.id_offset) * dp);
+            for (int v = 0; v < kRerankRows; ++v) {
+                const int64_t row = L.w_lab[min(c0 + NW * v, n - 1)] - a.id_offset;
+                r4[v] = reinterpret_cast<const float4*>(a.xb + row * dp);
+                xr[v] = a.xn[row];                      // loaded with the row, not after it
+            }
             rerank_dots<0>(q4, none, n4, lane, r4, acc);
 #pragma unroll
             for (int v = 0; v < kRerankRows; ++v) {
                 const int c = c0 + NW * v;
-                if (lane == 0 && c < n)
-                    L.w_key[c] = rerank_key(acc[v], B.qn, a.xn[L.w_lab[c] - a.id_offset], metric);
+                if (lane == 0 && c < n) L.w_key[c] = rerank_key(acc[v], B.qn, xr[v], metric);
             }
         }
         __syncthreads();
@@ -291,18 +310,34 @@ __device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int ite
     __syncthreads();
     const bool last = L.s_last != 0;
     __syncthreads();                                    // L reused below / by the next slice
-    if (!last) return false;
+    if (!last) return 0;
 
     // ---- the item's last slice: merge the S sorted slice lists (k each) in one wave — k rounds
     // of a wave u64 minimum over the S list heads, (ordered key bits | split-local label)
     // (a quadratic rank of the S x k survivors cost ~80 us at S = 32), certify, answer
     const float* sk_ = a.sc_key + (int64_t)item * S * k;
     const int64_t* sl_ = a.sc_lab + (int64_t)item * S * k;
+    // the S x k (<= kWideCap) slice lists staged in LDS by one round of independent sc1 loads:
+    // the merge's k rounds then read their heads from LDS (a dependent agent-scope load per
+    // round, ~1 us each across XCDs, was most of a one-query second chance)
+    for (int e = t; e < S * k; e += NT) {
+        L.w_lab[e] = __hip_atomic_load(sl_ + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        L.w_key[e] = __hip_atomic_load(sk_ + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the slices' floor, error ratio and overflow, loaded in the same round
+    unsigned tb = 0xffffffffu, rb = 0u, fb = 0u;
+    if (wave == 0 && lane < S) {
+        const unsigned* meta = a.sc_meta + ((int64_t)item * S + lane) * 4;
+        tb = __hip_atomic_load(meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rb = __hip_atomic_load(meta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fb = __hip_atomic_load(meta + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
     if (wave == 0) {
         auto head = [&](int p) -> uint64_t {
             if (lane >= S || p >= k) return ~0ull;
-            const int64_t lb = __hip_atomic_load(sl_ + lane * k + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const float kv = __hip_atomic_load(sk_ + lane * k + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t lb = L.w_lab[lane * k + p];
+            const float kv = L.w_key[lane * k + p];
             return lb < 0 ? ~0ull : ((uint64_t)key_bits_ordered(kv) << 32) | (uint32_t)(lb - a.id_offset);
         };
         L.o_key[lane] = INFINITY;                       // rounds after an exhausted merge: empty
@@ -322,13 +357,6 @@ __device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int ite
         }
         if (lane == 0) L.s_sk = sk;
         // the item's floor (min over slices), error ratio (max) and overflow (any)
-        unsigned tb = 0xffffffffu, rb = 0u, fb = 0u;
-        if (lane < S) {
-            const unsigned* meta = a.sc_meta + ((int64_t)item * S + lane) * 4;
-            tb = __hip_atomic_load(meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rb = __hip_atomic_load(meta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            fb = __hip_atomic_load(meta + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             tb = min(tb, (unsigned)__shfl_xor((int)tb, off, 64));
@@ -342,11 +370,11 @@ __device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int ite
         }
     }
     __syncthreads();
-    const unsigned tb = L.w_tau;
+    const unsigned tbm = L.w_tau;
     const int flag = L.s_flag;
     // +inf floor: no list dropped a row, so every row was a candidate and the slices hold all
     // that can matter
-    const float tauL = tb == 0xffffffffu ? INFINITY : key_from_ordered(tb);
+    const float tauL = tbm == 0xffffffffu ? INFINITY : key_from_ordered(tbm);
     const bool ok = flag == 0 && (tauL == INFINITY || (tauL - B.bound_a(tauL)) > (L.s_sk + B.bound_f(L.s_sk)));
     if (ok) {
         if (t < k) {
@@ -360,7 +388,7 @@ __device__ __forceinline__ bool second_chance_slice(const RerankArgs& a, int ite
     }
     __syncthreads();
     if (t == 0) a.sc_done[item] = 0;                    // ready for the next search's items
-    return true;
+    return ok ? 1 : 2;
 }
 
 }  // namespace imgrec

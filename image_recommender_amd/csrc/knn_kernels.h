@@ -50,8 +50,8 @@ struct RerankArgs {
     const float* xn;
     const float* xn_max;        // device scalar: max stored |x|^2
     int64_t id_offset;
-    const float* cd;            // nq x kc approximate keys, ascending
-    const int64_t* ci;          // nq x kc labels (id_offset applied), -1 = empty
+    float* cd;                  // nq x kc approximate keys, ascending (written here when l1_G > 0)
+    int64_t* ci;                // nq x kc labels (id_offset applied), -1 = empty
     int kc;
     int64_t nq;
     int k, metric;              // metric 1 = L2, otherwise inner product
@@ -62,8 +62,17 @@ struct RerankArgs {
     const float* q_resid;       // kModeBF16: |q - bf16(q)| per query (kModeI8: NULL, fp32 query)
     const float* xr_max;        // kModeBF16: device scalar, max over rows of |x - bf16(x)|;
                                 // kModeI8: max over rows of |x - s c| (the int8 copy's residual)
-    const float* floor;         // per query: smallest key any row outside the candidates can
+    float* floor;               // per query: smallest key any row outside the candidates can
                                 // have besides the K'-th candidate's (merge "floor"), or NULL
+    // the candidate merge's second level fused into the rerank (launch_merge_candidates with
+    // defer_level2; small batches): per query l1_G lists of 16 (key, label) at l1_d / l1_i +
+    // q * l1_G * 16 and their floors at l1_floor + q * l1_G; wave 0 selects the kc best and writes
+    // them to cd / ci and the floor to floor (the second chance reads them).  0 = cd / ci / floor
+    // are the inputs.
+    const float* l1_d = nullptr;
+    const int64_t* l1_i = nullptr;
+    const float* l1_floor = nullptr;
+    int l1_G = 0;
     float* D;
     int64_t* I;
     int* stats;                 // this chunk's device counters (zero on entry): [0] queries left
@@ -217,10 +226,15 @@ hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, 
 // own lane lists can have (+inf when nothing was dropped).
 // ws_*: two-level workspace for more than 64 lists per query (nq * ceil(nlists/64) * kout entries,
 // nq * ceil(nlists/64) floors), may be NULL when nlists <= 64.
+// l1_G (optional): when non-NULL and the merge takes two levels of which the first keeps 16 per
+// group, with at most 32 groups (one level-1 entry per rerank thread), only level 1 runs and
+// *l1_G = its group count (the rerank then selects the kout best from ws_*: RerankArgs::l1_G);
+// otherwise *l1_G = 0 and D / I / floor hold the result.
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,
                                    int64_t id_offset, float* D, int64_t* I, float* floor,
-                                   float* ws_d, int64_t* ws_i, float* ws_floor, hipStream_t st);
+                                   float* ws_d, int64_t* ws_i, float* ws_floor, hipStream_t st,
+                                   int* l1_G = nullptr);
 hipError_t launch_fill_empty(float* D, int64_t* I, int64_t n, int metric, hipStream_t st);
 // multi-device index: dst[i] = start + i, and labels through a shard's local -> global map
 // (I[i] = lmap[I[i]] + offset, -1 kept)

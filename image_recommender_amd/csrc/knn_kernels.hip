@@ -675,7 +675,9 @@ __device__ __forceinline__ void merge_query_wave(const float* __restrict__ cd,
 //      (or takes ticket 0 when none was queued) is the planner;
 //   2. the planner folds the stats, gathers the uncertified queries (fail_list) into fq / fqn
 //      (zero rows up to a multiple of 32), zeroes the per-query-block tickets and publishes
-//      ctl[2] = 1; everyone else waits for it (the planner is running: it completed an item);
+//      ctl[2] = count + 1 (at once when count = 0: nothing to gather); everyone else waits for
+//      it (the planner is running: it completed an item).  With one item its finisher is the
+//      planner without the ctl[1] count;
 //   3. exact (2,1)-tile items (query block, row split) are claimed from ctl[3]; the workgroup
 //      that finishes a query block's last split merges that block's lists into the rows
 //      fail_list[q] of D / I.
@@ -708,6 +710,7 @@ cert_tail_kernel(const TailArgs a) {
     }
     // ---- 1. second chance ----------------------------------------------------------------
     bool planner = false;
+    int known = -1;                             // the re-run count, when the planner knows it
     if (n_chance > 0) {
         // units = (item, slice), claimed from ctl[0]; the workgroup that finishes an item's last
         // slice counts the item in ctl[1]
@@ -718,9 +721,14 @@ cert_tail_kernel(const TailArgs a) {
             const int unit = s_val;
             __syncthreads();
             if (unit >= n_chance * S) break;
-            const bool finished = second_chance_slice<kTailWaves>(a.r, unit / S, unit % S,
-                                                                  *reinterpret_cast<SecondChanceLDS*>(smem));
-            if (!finished) continue;
+            const int res = second_chance_slice<kTailWaves>(a.r, unit / S, unit % S,
+                                                            *reinterpret_cast<SecondChanceLDS*>(smem));
+            if (res == 0) continue;
+            if (n_chance == 1) {                // the only item: its finisher plans, no count;
+                planner = true;                 // its outcome is the chunk's re-run count (the
+                known = res == 2 ? 1 : 0;       // rerank queues every failure for the chance)
+                continue;
+            }
             wg_release_stores();
             if (t == 0) {
                 const int done = lane0_release_add(ctl + 1);
@@ -738,9 +746,14 @@ cert_tail_kernel(const TailArgs a) {
         __syncthreads();
     }
     // ---- 2. plan + query gather (one workgroup) ------------------------------------------
+    int count;
     if (planner) {
-        const int count = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        count = known >= 0 ? known : __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int nqb = (count + 31) / 32;
+        // nothing to re-run: release the waiters at once (they read nothing the planner writes
+        // below; ctl[2] = count + 1 carries the count, saving each waiter a reload of sp)
+        if (count == 0 && t == 0) __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (count > 0) wg_release_stores();     // this workgroup's fail_list stores (one item)
         if (t == 0) {
             int* acc = a.stat + 8;
             acc[0] = a.first ? count : acc[0] + count;
@@ -762,11 +775,12 @@ cert_tail_kernel(const TailArgs a) {
             for (int j = lane; j < a.dp; j += 64) o[j] = s[j];
             if (lane == 0) a.fqn[row] = a.qnorm[src];
         }
+        if (count == 0) return;
         wg_release_stores();
         if (t == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctl + 2, count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             lane0_acquire();                    // this CU's L1 holds no stale copy of fq either
         }
         __syncthreads();
@@ -774,20 +788,20 @@ cert_tail_kernel(const TailArgs a) {
         if (t == 0) {
             // the planner is running (it completed an item or took ticket 0); the bound only
             // turns a broken invariant into a reported error (stats bit) instead of a hang
-            int spins = 0;
+            int spins = 0, c2;
             s_val = 0;
-            while (__hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            while ((c2 = __hip_atomic_load(ctl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1 << 26)) { s_val = 1; break; }
+                if (++spins > (1 << 26)) break;
             }
-            if (s_val) atomicOr(a.stat + 11, 1);
-            lane0_acquire();
+            if (c2 == 0) atomicOr(a.stat + 11, 1);
+            else if (c2 > 1) lane0_acquire();
+            s_val = c2 - 1;                     // -1: timed out
         }
         __syncthreads();
-        if (s_val) return;
+        count = s_val;
+        if (count <= 0) return;
     }
-    const int count = __hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (count == 0) return;
     // ---- 3. exact re-run: (query block, row split) items, merged by each block's last split ----
     const int nqb = (count + 31) / 32;
     const int nsplit = max(1, min((int)gridDim.x / nqb, a.ntiles));
@@ -938,10 +952,8 @@ hipError_t launch_merge_strided(const float* cd, const int64_t* ci, int64_t nq, 
 }
 
 // Candidate merge when every lane holds at most one sorted input list (<= 64 lists per query):
-// no insertion, the lane's list is its queue.  Entries are packed into one 64-bit value
-// (order-preserving key bits | local row), so each of the kout rounds is one wave u64 minimum
-// (wave_min_u64); the winning lane (unique: a row sits in one list) pops its head.
-// (wave_sum_i32 / wave_excl_scan_i32: wave_ops.h)
+// entries packed into one 64-bit value (order-preserving key bits | local row), the kout
+// smallest found by a wave select (wave_ops.h).
 
 // A query's nlists lists may be split into G groups of <= 64 (two-level merge): wave s handles
 // group s % G of query s / G; floor_in (optional, G per output row of the previous level) is
@@ -980,62 +992,15 @@ cand_merge_lane_kernel(const float* __restrict__ cd, const int64_t* __restrict__
     for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
     if (lane == 0) floor_out[sq] = fl;
 
-    // Output = the K = min(kout, valid) smallest packed values.  T, the K-th smallest, is found
-    // bit by bit (count of entries <= a trial value, summed over the wave): 32 steps over the key
-    // bits, and the 32 row bits only when the K-th key is tied across the cut.  Each lane's
-    // entries <= T (a prefix of its sorted list) go to LDS slots from an exclusive scan; a lane's
-    // output position is its value's rank among the K (values are distinct: a row sits in one
-    // list).
-    auto count_le = [&](uint64_t x) __attribute__((always_inline)) {
-        int c = 0;
-#pragma unroll
-        for (int p = 0; p < KIN; ++p) c += v[p] <= x ? 1 : 0;
-        return c;
-    };
-    int nvl = 0;
-    uint64_t vmin = kEmpty, vmax = 0;
-#pragma unroll
-    for (int p = 0; p < KIN; ++p) {
-        const bool val = v[p] != kEmpty;
-        nvl += val ? 1 : 0;
-        vmin = v[p] < vmin ? v[p] : vmin;
-        vmax = (val && v[p] > vmax) ? v[p] : vmax;
-    }
-    const int K = min(kout, wave_sum_i32(nvl));
-    uint64_t T = 0;
-    if (K > 0) {
-        // T lies in [min, max] of the valid values: the bits above their highest difference are
-        // common, so the select starts below them (keys of one query sit in a narrow range)
-        vmin = wave_min_u64(vmin);
-        vmax = ~wave_min_u64(~vmax);
-        const int hb = vmin == vmax ? -1 : 63 - __builtin_clzll(vmin ^ vmax);
-        uint64_t prefix = hb < 0 ? vmin : (hb >= 63 ? 0 : vmin & ~((2ull << hb) - 1));
-        for (int b = min(hb, 63); b >= 32; --b) {
-            const uint64_t lo = prefix | ((1ull << b) - 1);
-            if (wave_sum_i32(count_le(lo)) < K) prefix |= 1ull << b;
-        }
-        T = prefix | 0xffffffffull;
-        if (wave_sum_i32(count_le(T)) > K) {                   // the K-th key is tied: rows decide
-            for (int b = min(hb, 31); b >= 0; --b) {
-                const uint64_t lo = prefix | ((1ull << b) - 1);
-                if (wave_sum_i32(count_le(lo)) < K) prefix |= 1ull << b;
-            }
-            T = prefix;
-        }
-    }
-    __shared__ uint64_t sel[4][64];
-    uint64_t* buf = sel[threadIdx.x >> 6];
-    const int c = K > 0 ? count_le(T) : 0;
-    const int base = wave_excl_scan_i32(c);
-#pragma unroll
-    for (int p = 0; p < KIN; ++p)
-        if (p < c) buf[base + p] = v[p];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+    // the leading-entry bound + survivor ranks (wave_select_sorted): the list heads for
+    // kout <= 16 (level 1 of the two-level merge), the first two entries of every list above
+    uint64_t mine = 0;
+    int rank = 0;
+    __shared__ uint64_t sel[4][128 + 192];
+    uint64_t* const buf = sel[threadIdx.x >> 6];
+    const int K = kout <= 16 ? wave_select_sorted<KIN, 1, 256>(v, kout, buf, mine, rank)
+                             : wave_select_sorted<KIN, 2, 192>(v, kout, buf, mine, rank);
     if (lane < K) {
-        const uint64_t mine = buf[lane];
-        int rank = 0;
-        for (int j = 0; j < K; ++j) rank += buf[j] < mine ? 1 : 0;
         D[sq * kout + rank] = key_from_ordered((uint32_t)(mine >> 32));
         I[sq * kout + rank] = (int64_t)(uint32_t)mine + id_offset;
     } else if (lane < kout) {
@@ -1180,7 +1145,9 @@ cand_merge_block_kernel(const float* __restrict__ cd, const int64_t* __restrict_
 hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t nq, int nlists,
                                    int kin, int64_t stride_q, int64_t stride_l, int kout,
                                    int64_t id_offset, float* D, int64_t* I, float* floor,
-                                   float* ws_d, int64_t* ws_i, float* ws_floor, hipStream_t st) {
+                                   float* ws_d, int64_t* ws_i, float* ws_floor, hipStream_t st,
+                                   int* l1_G) {
+    if (l1_G) *l1_G = 0;
     if (nq <= 0) return hipSuccess;
     if (kout <= 0 || kout > 64 || !floor) return hipErrorInvalidValue;
     const int G = (nlists + 63) / 64;
@@ -1213,6 +1180,10 @@ hipError_t launch_merge_candidates(const float* cd, const int64_t* ci, int64_t n
             else IMGREC_CAND_LANE(16, nsub, nlists, G, stride_q, stride_l, 16, nullptr, 0, ws_d, ws_i, ws_floor);
             hipError_t e1 = hipGetLastError();
             if (e1 != hipSuccess) return e1;
+            if (l1_G && 16 * G <= kRerankWaves * 64) {   // level 2 in the rerank (an entry a thread)
+                *l1_G = G;
+                return hipSuccess;
+            }
             cd_ = ws_d;
             ci_ = ws_i;
             IMGREC_CAND_LANE(16, nq, G, 1, (int64_t)G * 16, 16, kout, ws_floor, G, D, I, floor);

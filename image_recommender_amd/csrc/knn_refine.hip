@@ -207,10 +207,76 @@ rerank_certify_kernel(const RerankArgs a) {
     const int64_t id_offset = a.id_offset;
     // the certificate tail kernel's grid-barrier counters start from zero (it runs next)
     if (a.tail_ctl && blockIdx.x == 0 && threadIdx.x < 4) a.tail_ctl[threadIdx.x] = 0;
-    const float* __restrict__ cd = a.cd;
-    const int64_t* __restrict__ ci = a.ci;
-    const int64_t lab = lane < kc ? ci[q * kc + lane] : (int64_t)-1;
-    const float ak = lane < kc ? cd[q * kc + lane] : INFINITY;   // approximate key, ascending
+    // exact fp32 keys of the prefix (below): candidate c goes to wave c % kRerankWaves; the query
+    // row is loaded first (while wave 0 runs the fused merge level)
+    const int n4 = dp / 4;
+    const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
+    float4 qr[IT > 0 ? IT : 1];
+    if constexpr (IT > 0) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int i = lane + 64 * it;
+            qr[it] = i < n4 ? q4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    // the candidate merge's second level (RerankArgs::l1_G): the query's E = 16 l1_G level-1
+    // entries (<= one per thread) packed (order-preserving key bits | row) in LDS; each thread
+    // ranks its entry against all E (broadcast LDS reads; entries are distinct: a row sits in
+    // one list) and the kc smallest land at their ranks — for this kernel (LDS) and the second
+    // chance (global).  (The wave threshold select of cand_merge_lane_kernel took ~10 us here:
+    // 32 dependent wave-sum steps in one wave while seven waited.)
+    const bool fused = a.l1_G > 0;
+    __shared__ float s_mkey[64];
+    __shared__ int64_t s_mlab[64];
+    __shared__ __attribute__((aligned(16))) uint64_t s_ent[kRerankWaves * 64];
+    __shared__ float s_floor;
+    if (fused) {
+        constexpr uint64_t kEmpty = ~0ull;
+        const int t = threadIdx.x, G = a.l1_G, E = 16 * G;
+        const float* ld = a.l1_d + q * E;
+        const int64_t* li = a.l1_i + q * E;
+        uint64_t mine = kEmpty;
+        if (t < E) {
+            const int64_t lb = li[t];
+            if (lb >= 0) mine = ((uint64_t)key_bits_ordered(ld[t]) << 32) | (uint32_t)(lb - id_offset);
+            s_ent[t] = mine;
+        }
+        if (wave == 0) {                                // floor: the level-1 floors and the last
+            float fl = INFINITY;                        // key of every full level-1 list
+            if (lane < G) {
+                fl = a.l1_floor[q * G + lane];
+                if (li[16 * lane + 15] >= 0) fl = fminf(fl, ld[16 * lane + 15]);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+            if (lane == 0) s_floor = fl;
+        }
+        const int nv = __syncthreads_count(mine != kEmpty);
+        const int K = min(kc, nv);
+        if (mine != kEmpty) {
+            int r = 0;
+            const ulonglong2* e2 = reinterpret_cast<const ulonglong2*>(s_ent);
+#pragma unroll 4
+            for (int j = 0; j < E / 2; ++j) {
+                const ulonglong2 p = e2[j];
+                r += (p.x < mine ? 1 : 0) + (p.y < mine ? 1 : 0);
+            }
+            if (r < K) {
+                const float kv = key_from_ordered((uint32_t)(mine >> 32));
+                const int64_t lb = (int64_t)(uint32_t)mine + id_offset;
+                s_mkey[r] = kv; s_mlab[r] = lb;
+                a.cd[q * kc + r] = kv; a.ci[q * kc + r] = lb;
+            }
+        }
+        if (t >= K && t < kc) {
+            s_mkey[t] = FLT_MAX; s_mlab[t] = -1;
+            a.cd[q * kc + t] = FLT_MAX; a.ci[q * kc + t] = -1;
+        }
+        if (t == 0) a.floor[q] = s_floor;
+        __syncthreads();
+    }
+    const int64_t lab = lane < kc ? (fused ? s_mlab[lane] : a.ci[q * kc + lane]) : (int64_t)-1;
+    const float ak = lane < kc ? (fused ? s_mkey[lane] : a.cd[q * kc + lane]) : INFINITY;  // ascending
     const bool valid = lab >= 0;
     const int nvalid = __popcll(__ballot(valid));               // valid candidates come first
     const QueryBounds B(a, q);
@@ -224,17 +290,6 @@ rerank_certify_kernel(const RerankArgs a) {
         m = __popcll(__ballot(valid && ak <= thr));
     }
 
-    // exact fp32 keys of the prefix: candidate c goes to wave c % kRerankWaves
-    const int n4 = dp / 4;
-    const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
-    float4 qr[IT > 0 ? IT : 1];
-    if constexpr (IT > 0) {
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int i = lane + 64 * it;
-            qr[it] = i < n4 ? q4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    }
     auto row_of = [&](int c) {
         const int lo32 = __shfl((int)(lab & 0xffffffff), c, 64);
         const int hi32 = __shfl((int)(lab >> 32), c, 64);
@@ -311,9 +366,12 @@ rerank_certify_kernel(const RerankArgs a) {
     // certificate: tau = smallest approximate key a row outside the prefix can have — the K'-th
     // candidate's (when the set is full), the merge floor (rows dropped by full lists) and the
     // first candidate left out of the prefix; +inf means every row was reranked
-    const int64_t lab_tau = ci[q * kc + kc - 1];
-    float tau = (lab_tau >= 0 && nvalid >= kc) ? cd[q * kc + kc - 1] : INFINITY;
-    if (a.floor) tau = fminf(tau, a.floor[q]);
+    const int lo_tau = __shfl((int)(lab & 0xffffffff), kc - 1, 64);
+    const int hi_tau = __shfl((int)(lab >> 32), kc - 1, 64);
+    const int64_t lab_tau = ((int64_t)hi_tau << 32) | (uint32_t)lo_tau;
+    float tau = (lab_tau >= 0 && nvalid >= kc) ? __shfl(ak, kc - 1, 64) : INFINITY;
+    if (fused) tau = fminf(tau, s_floor);
+    else if (a.floor) tau = fminf(tau, a.floor[q]);
     const float a_out = __shfl(ak, min(m, 63), 64);
     if (m < nvalid) tau = fminf(tau, a_out);
     bool failed = false;                            // tau = +inf: every row was reranked
@@ -386,6 +444,8 @@ hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
     if (a.kc > 64 || a.k > a.kc || a.k > 64 || a.dp % 4 != 0 || !a.stats || !a.fail_list)
+        return hipErrorInvalidValue;
+    if (a.l1_G > 0 && (16 * a.l1_G > kRerankWaves * 64 || !a.l1_d || !a.l1_i || !a.l1_floor || !a.floor))
         return hipErrorInvalidValue;
     if (a.raw_d && (!a.raw_i || !a.chance_list || a.raw_km < a.k || a.raw_lists <= 0))
         return hipErrorInvalidValue;

@@ -125,7 +125,8 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
             const int v = e ? std::atoi(e) : 0;
             return v > 0 ? v : 64;
         }();
-        // (<= 64: the last slice's merge reads the slice heads from the lanes of one wave)
+        // (<= 64: the last slice's merge reads the slice heads from the lanes of one wave;
+        // S k <= 1024 = kWideCap, knn_certify.h: it stages the S lists of k in LDS)
         r.sc_slices = std::max(1, std::min({kSlices, 64, r.raw_lists, 1024 / k}));
         const size_t ns = (size_t)nq * r.sc_slices * k;
         if ((rc = grow(&ix->sc_key, &ix->sc_key_cap, ns)) != KNN_OK) return rc;
@@ -170,6 +171,18 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     ix->stat_valid = true;
     ix->last_split_queries += nq;
     return KNN_OK;
+}
+
+// The candidate merge's second level inside the rerank kernel (one launch fewer: ~10 us at
+// nq = 1, where it is one wave's select behind a kernel boundary) while the batch leaves the rerank
+// at most one workgroup per CU; larger batches keep the separate level-2 launch (its 4-wave blocks
+// do not idle seven waves of each rerank workgroup behind the select).  IMGREC_MERGE_FUSE=0: off.
+bool fuse_merge_level2(const knn_index* ix, int64_t nq) {
+    static const bool on = [] {
+        const char* e = std::getenv("IMGREC_MERGE_FUSE");
+        return !(e && *e == '0');
+    }();
+    return on && nq <= ix->cus;
 }
 
 // Sibling lockstep of the 256 x 256 bf16 kernel (TileArgs::sync): IMGREC_B16W_SYNC_LAG = the
@@ -231,9 +244,11 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
         if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
         if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
     }
+    int l1G = 0;
     KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
                                     ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
-                                    ix->mws_d, ix->mws_i, ix->mws_f, st));
+                                    ix->mws_d, ix->mws_i, ix->mws_f, st,
+                                    fuse_merge_level2(ix, nq) ? &l1G : nullptr));
     RerankArgs r{};
     r.mode = kModeBF16;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
@@ -242,6 +257,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
     r.c_trunc = a.ib > 0 ? (float)std::ldexp(1.0, a.ib - 23) : 0.f;
     r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
+    if (l1G > 0) { r.l1_d = ix->mws_d; r.l1_i = ix->mws_i; r.l1_floor = ix->mws_f; r.l1_G = l1G; }
     r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = km;
     r.raw_stride_q = p.ncand;
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
@@ -280,9 +296,11 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
         if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
         if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
     }
+    int l1G = 0;
     KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, p.km, p.ncand, p.km, kc,
                                     ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
-                                    ix->mws_d, ix->mws_i, ix->mws_f, st));
+                                    ix->mws_d, ix->mws_i, ix->mws_f, st,
+                                    fuse_merge_level2(ix, nq) ? &l1G : nullptr));
     RerankArgs r{};
     r.mode = kModeI8;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
@@ -291,6 +309,7 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
     r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
     r.c_trunc = 0.f;
     r.q_resid = ix->q8r; r.xr_max = ix->x8r_max; r.floor = ix->floor;
+    if (l1G > 0) { r.l1_d = ix->mws_d; r.l1_i = ix->mws_i; r.l1_floor = ix->mws_f; r.l1_G = l1G; }
     r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = p.km;
     r.raw_stride_q = p.ncand;
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);

@@ -93,7 +93,7 @@ for st in "$@"; do
       bash tools/trace_step.sh $TAG/trace_$(echo "$arg" | tr ' -' '__') $arg > $OUT/trace.log 2>&1 || fail trace $OUT/trace.log
       cat $OUT/trace.log ;;
     probe)
-      CFG=${arg:-2} timeout -k 10 300 python tools/i8_cfg2_probe.py > $OUT/probe_cfg${arg:-2}.jsonl 2> $OUT/probe_cfg${arg:-2}.err || fail probe $OUT/probe_cfg${arg:-2}.err
+      CFG=${arg:-2} FENCE=${FENCE:-eager} timeout -k 10 300 python tools/i8_cfg2_probe.py > $OUT/probe_cfg${arg:-2}.jsonl 2> $OUT/probe_cfg${arg:-2}.err || fail probe $OUT/probe_cfg${arg:-2}.err
       cat $OUT/probe_cfg${arg:-2}.jsonl ;;
     stamps)
       c=${arg%%:*}; c=${c:-3}; lib=libimgrec_stamps.so; [ "${arg#*:}" != "$arg" ] && lib=${arg#*:}

@@ -1,5 +1,6 @@
 """Where the int8 single-query search spends its time on config 2 (1M x 768 L2): certificate
-counts and per-search time for the int8 and bf16 paths over 32 queries (measurement tool)."""
+counts and per-search time for the int8 and bf16 paths over 32 queries (measurement tool).
+FENCE=lazy: the index's lazy fence (Index.set_fence_mode; no event record per search)."""
 import json
 import os
 import sys
@@ -23,6 +24,9 @@ for blk in bench.gen_rows(torch, cfg, cent, 0, cfg["rows"], dev, cid):
     shard.add_local(blk)
 q = bench.gen_queries(torch, cfg, cent, 32, dev, cid)
 idx = shard.index
+fence = os.environ.get("FENCE", "eager")
+if fence == "lazy":
+    idx.set_fence_mode(True)
 for mode in ("i8", "bf16"):
     idx.search_mode = mode
     tot = {"second_chance": 0, "exact_reruns": 0}
@@ -40,5 +44,5 @@ for mode in ("i8", "bf16"):
         tot["second_chance"] += st["second_chance"]
         tot["exact_reruns"] += st["exact_reruns"]
     ts.sort()
-    print(json.dumps({"config": cid, "mode": mode, "median_ms": ts[16] * 1e3, "max_ms": ts[-1] * 1e3,
+    print(json.dumps({"config": cid, "mode": mode, "fence": fence, "median_ms": ts[16] * 1e3, "max_ms": ts[-1] * 1e3,
                       "min_ms": ts[0] * 1e3, **tot}), flush=True)
