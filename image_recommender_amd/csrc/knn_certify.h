@@ -22,6 +22,18 @@ __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
 
 constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
 
+#ifdef IMGREC_TAIL_STAMPS
+// diagnostic build only (tools/tail_stamps.py): s_memrealtime (100 MHz, one clock for every
+// XCD) per workgroup of the certificate tail
+// at fixed points (slot: 0 entry, 1 first claim, 2 slice filtered, 3 slice reranked, 4 slice
+// counted, 5 item merged, 6 plan published / seen, 7 exit); 1024 workgroups x 8 slots
+__device__ unsigned long long g_tail_stamps[1024 * 8];
+#define TAIL_STAMP(slot) do { if (threadIdx.x == 0 && blockIdx.x < 1024) \
+    g_tail_stamps[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TAIL_STAMP(slot) do {} while (0)
+#endif
+
 // Error bounds of one query's certificate (DESIGN.md "bf16 path" / "Split path").
 struct QueryBounds {
     float qn, xm, nn, e_ip, c_fp, c_trunc;
@@ -247,6 +259,7 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
         if (t + u * NT < ne) take(t + u * NT, pl[u], pv[u]);
     for (int j = t + kPre * NT; j < ne; j += NT) take(j, ri[entry(j)], rd[entry(j)]);
     __syncthreads();
+    TAIL_STAMP(2);
     const int n = L.w_n;
     const bool overflow = n > kWideCap;
     float* const ok_ = a.sc_key + ((int64_t)item * S + slice) * k;
@@ -270,6 +283,7 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
             }
         }
         __syncthreads();
+        TAIL_STAMP(3);
         // this slice's k best by (key, label) (labels are distinct: a row sits in one list);
         // the observed error / bound goes to the chunk's maximum once per workgroup (one
         // same-address global atomic per reranked entry serialised the slices: ~100 us)
@@ -310,6 +324,7 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
     __syncthreads();
     const bool last = L.s_last != 0;
     __syncthreads();                                    // L reused below / by the next slice
+    TAIL_STAMP(4);
     if (!last) return 0;
 
     // ---- the item's last slice: merge the S sorted slice lists (k each) in one wave — k rounds
@@ -388,6 +403,7 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
     }
     __syncthreads();
     if (t == 0) a.sc_done[item] = 0;                    // ready for the next search's items
+    TAIL_STAMP(5);
     return ok ? 1 : 2;
 }
 

@@ -696,6 +696,7 @@ cert_tail_kernel(const TailArgs a) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     int* const sp = a.stat + 4 * a.parity;
     int* const ctl = a.r.tail_ctl;
+    TAIL_STAMP(0);
     const int n_chance = sp[3];                 // final: the rerank kernel has completed
     if (n_chance == 0 && sp[0] == 0) {          // the common case: every query certified
         if (blockIdx.x == 0 && t == 0) {
@@ -720,6 +721,7 @@ cert_tail_kernel(const TailArgs a) {
             __syncthreads();
             const int unit = s_val;
             __syncthreads();
+            TAIL_STAMP(1);
             if (unit >= n_chance * S) break;
             const int res = second_chance_slice<kTailWaves>(a.r, unit / S, unit % S,
                                                             *reinterpret_cast<SecondChanceLDS*>(smem));
@@ -753,6 +755,7 @@ cert_tail_kernel(const TailArgs a) {
         // nothing to re-run: release the waiters at once (they read nothing the planner writes
         // below; ctl[2] = count + 1 carries the count, saving each waiter a reload of sp)
         if (count == 0 && t == 0) __hip_atomic_store(ctl + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        TAIL_STAMP(6);
         if (count > 0) wg_release_stores();     // this workgroup's fail_list stores (one item)
         if (t == 0) {
             int* acc = a.stat + 8;
@@ -775,7 +778,7 @@ cert_tail_kernel(const TailArgs a) {
             for (int j = lane; j < a.dp; j += 64) o[j] = s[j];
             if (lane == 0) a.fqn[row] = a.qnorm[src];
         }
-        if (count == 0) return;
+        if (count == 0) { TAIL_STAMP(7); return; }
         wg_release_stores();
         if (t == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -799,8 +802,9 @@ cert_tail_kernel(const TailArgs a) {
             s_val = c2 - 1;                     // -1: timed out
         }
         __syncthreads();
+        TAIL_STAMP(6);
         count = s_val;
-        if (count <= 0) return;
+        if (count <= 0) { TAIL_STAMP(7); return; }
     }
     // ---- 3. exact re-run: (query block, row split) items, merged by each block's last split ----
     const int nqb = (count + 31) / 32;
@@ -832,6 +836,16 @@ cert_tail_kernel(const TailArgs a) {
         __syncthreads();                        // s_val and the LDS ring reused by the next item
     }
 }
+
+#ifdef IMGREC_TAIL_STAMPS
+extern "C" int knn_tail_stamps_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(imgrec::g_tail_stamps), sizeof(imgrec::g_tail_stamps));
+}
+extern "C" int knn_tail_stamps_clear() {
+    static unsigned long long zero[1024 * 8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(imgrec::g_tail_stamps), zero, sizeof(zero));
+}
+#endif
 
 hipError_t launch_cert_tail(const TailArgs& a, int grid, hipStream_t st) {
     if (grid <= 0 || !a.r.tail_ctl || !a.ticket || a.dp % kTailBK != 0) return hipErrorInvalidValue;

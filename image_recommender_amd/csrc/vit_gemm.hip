@@ -67,15 +67,18 @@ static_assert(kBKW == 32 && kCPR == 8 && kRPP == 8 && kRPB == 2, "stage geometry
 static_assert(kLPW == 8, "pieces go out in two dma4x groups");
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 
+// The sigmoid forms divide by v_rcp_f32 (1 ulp) instead of the IEEE division sequence (scale,
+// Newton steps, fixup: ~10 VALU per element — most of fc1's epilogue); the result is rounded to
+// bf16 (2^-9) right after, so the ulp never shows.
 template <int ACT>
 __device__ __forceinline__ float activate(float x) {
     if constexpr (ACT == VIT_ACT_GELU_ERF) return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
     if constexpr (ACT == VIT_ACT_GELU_TANH) {
         // 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3)
         const float u = 0.7978845608028654f * fmaf(0.044715f * x * x, x, x);
-        return x / (1.f + __expf(-2.f * u));
+        return x * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * u));
     }
-    if constexpr (ACT == VIT_ACT_QUICK_GELU) return x / (1.f + __expf(-1.702f * x));
+    if constexpr (ACT == VIT_ACT_QUICK_GELU) return x * __builtin_amdgcn_rcpf(1.f + __expf(-1.702f * x));
     return x;
 }
 

@@ -22,6 +22,8 @@
 #   stamps=CFG[:LIB] per-tile stage-loop / epilogue cycles of the 256 x 256 bf16 kernel on bench
 #                   config CFG (lib/LIB, default libimgrec_stamps.so: tools/build_variants.sh stamps
 #                   -DIMGREC_B16_STAMPS)
+#   tailstamps=CFG  tools/tail_stamps.py: certificate-tail workgroup timestamps of one-query second
+#                   chances (lib/libimgrec_tailstamps.so: build_variants.sh tailstamps -DIMGREC_TAIL_STAMPS)
 #   ab=LIB          A/B of lib/libimgrec.so and lib/LIB: per-step and kernel ms on cfg2 and cfg3
 #                   (profile-only, twice alternating) -> ab_LIB.txt
 # Extra bench arguments for every bench stage: BENCH_ARGS.
@@ -100,6 +102,9 @@ for st in "$@"; do
       IMGREC_LIB_NAME=$lib IMGREC_STAMPS_CFG=$c IMGREC_STAMPS_FN=knn_b16w_stamps_read timeout -k 10 300 python tools/b16_stamps.py \
         > $OUT/stamps_cfg${c}_$lib.json 2> $OUT/stamps_cfg${c}_$lib.err || fail stamps $OUT/stamps_cfg${c}_$lib.err
       cat $OUT/stamps_cfg${c}_$lib.err ;;
+    tailstamps)
+      CFG=${arg:-2} timeout -k 10 300 python tools/tail_stamps.py > $OUT/tail_stamps_cfg${arg:-2}.jsonl 2> $OUT/tail_stamps.err || fail tailstamps $OUT/tail_stamps.err
+      tail -3 $OUT/tail_stamps_cfg${arg:-2}.jsonl ;;
     ab)
       for rep in 1 2; do
         for lib in libimgrec.so $arg; do
