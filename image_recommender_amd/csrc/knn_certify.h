@@ -207,13 +207,13 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
 
 template <int NW>
 __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item, int slice,
-                                                   SecondChanceLDS& L) {
+                                                   SecondChanceLDS& L, int q_item0) {
     constexpr int NT = NW * 64;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc, S = a.sc_slices;
     const int n4 = dp / 4;
     const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
-    const int64_t q = a.chance_list[item];
+    const int64_t q = item == 0 ? q_item0 : a.chance_list[item];    // item 0's: loaded at entry
     const float* rd = a.raw_d + q * a.raw_stride_q;
     const int64_t* ri = a.raw_i + q * a.raw_stride_q;
     const int km = a.raw_km;
@@ -335,9 +335,26 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
     // the S x k (<= kWideCap) slice lists staged in LDS by one round of independent sc1 loads:
     // the merge's k rounds then read their heads from LDS (a dependent agent-scope load per
     // round, ~1 us each across XCDs, was most of a one-query second chance)
-    for (int e = t; e < S * k; e += NT) {
-        L.w_lab[e] = __hip_atomic_load(sl_ + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        L.w_key[e] = __hip_atomic_load(sk_ + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (unrolled: every load in flight before the first LDS store — a rolled loop waited for each
+    // iteration's loads in turn, ~7 us of a one-query second chance, tools/tail_stamps.py)
+    constexpr int kStg = (kWideCap + NT - 1) / NT;
+    int64_t slb[kStg];
+    float skv[kStg];
+#pragma unroll
+    for (int u = 0; u < kStg; ++u) {
+        const int e = t + u * NT;
+        if (e < S * k) {
+            slb[u] = __hip_atomic_load(sl_ + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            skv[u] = __hip_atomic_load(sk_ + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kStg; ++u) {
+        const int e = t + u * NT;
+        if (e < S * k) {
+            L.w_lab[e] = slb[u];
+            L.w_key[e] = skv[u];
+        }
     }
     // the slices' floor, error ratio and overflow, loaded in the same round
     unsigned tb = 0xffffffffu, rb = 0u, fb = 0u;

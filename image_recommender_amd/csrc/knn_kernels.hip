@@ -698,6 +698,7 @@ cert_tail_kernel(const TailArgs a) {
     int* const ctl = a.r.tail_ctl;
     TAIL_STAMP(0);
     const int n_chance = sp[3];                 // final: the rerank kernel has completed
+    const int q_item0 = a.r.chance_list ? a.r.chance_list[0] : -1;   // in the same round trip
     if (n_chance == 0 && sp[0] == 0) {          // the common case: every query certified
         if (blockIdx.x == 0 && t == 0) {
             int* acc = a.stat + 8;
@@ -724,7 +725,7 @@ cert_tail_kernel(const TailArgs a) {
             TAIL_STAMP(1);
             if (unit >= n_chance * S) break;
             const int res = second_chance_slice<kTailWaves>(a.r, unit / S, unit % S,
-                                                            *reinterpret_cast<SecondChanceLDS*>(smem));
+                                                            *reinterpret_cast<SecondChanceLDS*>(smem), q_item0);
             if (res == 0) continue;
             if (n_chance == 1) {                // the only item: its finisher plans, no count;
                 planner = true;                 // its outcome is the chunk's re-run count (the
