@@ -79,13 +79,15 @@ struct QueryBounds {
     __device__ __forceinline__ float trunc(float a) const { return c_trunc * fabsf(a); }
 };
 
-// Exact fp32 dot products of one query with kRerankRows rows, one wave, lane-strided float4
-// chunks (x y z w FMAs) then a butterfly: a row's key has the same bits in every pass.
-// IT > 0: the query's chunks are in registers (qr); IT = 0: streamed with the rows.
-template <int IT>
+// Exact fp32 dot products of one query with R rows (default kRerankRows), one wave,
+// lane-strided float4 chunks (x y z w FMAs) then a butterfly: a row's key has the same bits in
+// every pass, whatever R.  IT > 0: the query's chunks are in registers (qr); IT = 0: streamed
+// with the rows.
+template <int IT, int R = kRerankRows>
 __device__ __forceinline__ void rerank_dots(const float4* __restrict__ q4, const float4 (&qr)[IT > 0 ? IT : 1],
-                                            int n4, int lane, const float4* const (&r4)[kRerankRows],
-                                            float (&acc)[kRerankRows]) {
+                                            int n4, int lane, const float4* const (&r4)[R],
+                                            float (&acc)[R]) {
+    constexpr int kRerankRows = R;
 #pragma unroll
     for (int v = 0; v < kRerankRows; ++v) acc[v] = 0.f;
     if constexpr (IT > 0) {

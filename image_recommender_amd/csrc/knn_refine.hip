@@ -296,19 +296,22 @@ rerank_certify_kernel(const RerankArgs a) {
         const int64_t l = ((int64_t)hi32 << 32) | (uint32_t)lo32;
         return reinterpret_cast<const float4*>(a.xb + (l - id_offset) * dp);
     };
-    // candidates [c_begin, c_end), kRerankWaves * kRerankRows rows in flight per round
-    auto rerank_range = [&](int c_begin, int c_end) {
-        for (int c0 = c_begin + wave; c0 < c_end; c0 += kRerankWaves * kRerankRows) {
-            const float4* r4[kRerankRows];
-            float acc[kRerankRows];
+    // the lane's own candidate's |x|^2, loaded up front (not after each round's dot products)
+    const float xn_own = valid ? a.xn[lab - id_offset] : 0.f;
+    // candidates [c_begin, c_end), kRerankWaves * R rows in flight per round
+    auto rerank_range = [&](int c_begin, int c_end, auto r_tag) {
+        constexpr int R = decltype(r_tag)::value;
+        for (int c0 = c_begin + wave; c0 < c_end; c0 += kRerankWaves * R) {
+            const float4* r4[R];
+            float acc[R];
 #pragma unroll
-            for (int v = 0; v < kRerankRows; ++v)
+            for (int v = 0; v < R; ++v)
                 r4[v] = row_of(min(c0 + kRerankWaves * v, c_end - 1));   // clamped: loads unconditional
-            rerank_dots<IT>(q4, qr, n4, lane, r4, acc);
+            rerank_dots<IT, R>(q4, qr, n4, lane, r4, acc);
 #pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
+            for (int v = 0; v < R; ++v) {
                 const int c = c0 + kRerankWaves * v;
-                if (lane == c && c < c_end) skey[c] = rerank_key(acc[v], B.qn, a.xn[lab - id_offset], metric);
+                if (lane == c && c < c_end) skey[c] = rerank_key(acc[v], B.qn, xn_own, metric);
             }
         }
     };
@@ -320,7 +323,7 @@ rerank_certify_kernel(const RerankArgs a) {
     // limit; its first candidate left out passes the certificate by construction.
     constexpr int P1 = kRerankWaves * kRerankRows;
     const int m1 = min(m, P1);
-    rerank_range(0, m1);
+    rerank_range(0, m1, std::integral_constant<int, kRerankRows>{});
     __syncthreads();
     if (m > m1) {
         if (m1 >= k) {                                  // (k > P1: the whole prefix, one phase)
@@ -334,7 +337,8 @@ rerank_certify_kernel(const RerankArgs a) {
             const int m2 = __popcll(__ballot(valid && lane < m && ak - B.bound_a(ak) <= lim));
             m = max(m1, m2);
         }
-        rerank_range(m1, m);
+        // (4 rows per wave in flight here measured no faster at one query: 23.4 vs 22.4 us)
+        rerank_range(m1, m, std::integral_constant<int, kRerankRows>{});
         __syncthreads();
     }
     if (wave != 0) return;
