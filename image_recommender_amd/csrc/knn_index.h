@@ -84,7 +84,9 @@ float b16_acc_coef(int dpb);
 // int8 small-batch pass (knn_i8.hip): batches of at most kI8MaxQ queries, K' = kB16Cand
 constexpr int kI8MaxQ = 8;
 float i8_acc_coef(int nblk);
-Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus);
+// wgpcu: int8 scan workgroups per CU (the split count is CUs x wgpcu); 0 = by batch size
+Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus, int wgpcu);
+constexpr int kI8WGPCUDefault = 0;
 constexpr int kB16Cand = 64;                   // K': candidates the bf16 pass hands to the rerank
 int b16_km(int k);
 
@@ -92,6 +94,11 @@ int b16_km(int k);
 
 struct knn_index {
     int d = 0, dp = 0, metric = KNN_METRIC_L2, device = 0, cus = 256;
+    // launch knobs read from the environment at creation (A/B and tests): the int8 scan's
+    // workgroups per CU (IMGREC_I8_WGPCU) and the merge's second level inside the rerank
+    // (IMGREC_MERGE_FUSE=0: off)
+    int i8_wgpcu = imgrec::kI8WGPCUDefault;
+    bool merge_fuse = true;
     int64_t ntotal = 0, cap = 0, id_offset = 0;
     bool trained = true;
     float* xb = nullptr;     // cap x dp

@@ -93,16 +93,11 @@ float i8_acc_coef(int nblk) {
 // (two 4-wave workgroups per CU are resident at the kernel's 222 VGPRs; three per CU, i.e. a
 // second partial round, measured faster at nq = 1 / 2: 0.366 / 0.375 vs 0.386 / 0.399 ms kernel,
 // profiles/r03/i8_small_batch/sweep.jsonl; IMGREC_I8_WGPCU overrides for measurements)
-static int i8_wgpcu() {
-    static const int v = [] {
-        const char* e = std::getenv("IMGREC_I8_WGPCU");
-        const int x = e ? std::atoi(e) : 0;
-        return x > 0 && x <= 16 ? x : 3;
-    }();
-    return v;
-}
-Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus) {
-    const int kI8WGPCU = i8_wgpcu();
+// Workgroups per CU of the int8 scan: 2 for one or two queries (fewer lists for the merge, and
+// the scan itself no slower: cfg2 one query 0.187 -> 0.182 ms), 3 from four queries on (cfg2 at
+// nq = 8: 0.406 ms with 2, 0.358 with 3) — profiles/r04/i8_wgpcu/.
+Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus, int wgpcu) {
+    const int kI8WGPCU = wgpcu > 0 ? wgpcu : (nq <= 2 ? 2 : 3);
     Plan p{};
     p.km = b16_km(k);
     p.wr = 1;

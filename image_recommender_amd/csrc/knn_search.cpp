@@ -176,13 +176,10 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
 // The candidate merge's second level inside the rerank kernel (one launch fewer: ~10 us at
 // nq = 1, where it is one wave's select behind a kernel boundary) while the batch leaves the rerank
 // at most one workgroup per CU; larger batches keep the separate level-2 launch (its 4-wave blocks
-// do not idle seven waves of each rerank workgroup behind the select).  IMGREC_MERGE_FUSE=0: off.
+// do not idle seven waves of each rerank workgroup behind the select).  IMGREC_MERGE_FUSE=0 at
+// index creation: off.
 bool fuse_merge_level2(const knn_index* ix, int64_t nq) {
-    static const bool on = [] {
-        const char* e = std::getenv("IMGREC_MERGE_FUSE");
-        return !(e && *e == '0');
-    }();
-    return on && nq <= ix->cus;
+    return ix->merge_fuse && nq <= ix->cus;
 }
 
 // Sibling lockstep of the 256 x 256 bf16 kernel (TileArgs::sync): IMGREC_B16W_SYNC_LAG = the
@@ -269,7 +266,7 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
              int64_t* I, hipStream_t st, bool timed, bool first) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = kB16Cand;
-    const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus);
+    const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus, ix->i8_wgpcu);
     int rc;
     if ((rc = ensure_i8(ix, st)) != KNN_OK) return rc;
     if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
@@ -420,7 +417,7 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         const bool b16 = !i8 && use_b16(ix, cn, k);
         const bool split = !i8 && !b16 && use_split(ix, cn, k);
         // padding: the query tile of the plan this chunk will run (and the exact re-run's 32)
-        const Plan p = i8 ? make_i8_plan(ix->ntotal, cn, k, ix->cus)
+        const Plan p = i8 ? make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu)
                      : b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                      : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                              : make_plan(ix->ntotal, cn, k, ix->cus);
