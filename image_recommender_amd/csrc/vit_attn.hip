@@ -87,26 +87,31 @@ attn_kernel(const uint16_t* __restrict__ qkv, int ntok, int heads, float scale_l
     const uint16_t* const base = qkv + (int64_t)b * ntok * tok_stride + (int64_t)h * kHD;
     const int64_t koff = (int64_t)heads * kHD, voff = 2 * koff;
 
-    // ---- K then V of this (image, head) into LDS, stored swizzled; rows >= ntok are zero
+    // ---- K and V of this (image, head) into LDS, stored swizzled; rows >= ntok are zero.  Every
+    // load of both is issued before the first LDS store (K's stores waiting on K's loads before V's
+    // loads went out cost one more HBM round trip per workgroup)
     {
         constexpr int kChunks = kRows * 8;
         constexpr int kPer = (kChunks + kWaves * 64 - 1) / (kWaves * 64);
+        uint4 rr[2][kPer];
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
             const int64_t moff = m == 0 ? koff : voff;
-            char* const dst = m == 0 ? sk : sv;
-            uint4 rr[kPer];
 #pragma unroll
             for (int j = 0; j < kPer; ++j) {
                 const int i = tid + j * kWaves * 64, r = i >> 3, c = i & 7;
                 // rows past the last token load the last token's row (in bounds) and store zeros
-                rr[j] = *reinterpret_cast<const uint4*>(base + (int64_t)min(r, ntok - 1) * tok_stride + 8 * c + moff);
-                if (r >= ntok) rr[j] = make_uint4(0u, 0u, 0u, 0u);
+                rr[m][j] = *reinterpret_cast<const uint4*>(base + (int64_t)min(r, ntok - 1) * tok_stride + 8 * c + moff);
+                if (r >= ntok) rr[m][j] = make_uint4(0u, 0u, 0u, 0u);
             }
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            char* const dst = m == 0 ? sk : sv;
 #pragma unroll
             for (int j = 0; j < kPer; ++j) {
                 const int i = tid + j * kWaves * 64, r = i >> 3, c = i & 7;
-                if (i < kChunks) *reinterpret_cast<uint4*>(dst + img_off(r, c)) = rr[j];
+                if (i < kChunks) *reinterpret_cast<uint4*>(dst + img_off(r, c)) = rr[m][j];
             }
         }
     }
