@@ -99,6 +99,7 @@ struct knn_index {
     // (IMGREC_MERGE_FUSE=0: off)
     int i8_wgpcu = imgrec::kI8WGPCUDefault;
     bool merge_fuse = true;
+    bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
     int64_t ntotal = 0, cap = 0, id_offset = 0;
     bool trained = true;
     float* xb = nullptr;     // cap x dp

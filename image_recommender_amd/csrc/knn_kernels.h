@@ -73,6 +73,8 @@ struct RerankArgs {
     const int64_t* l1_i = nullptr;
     const float* l1_floor = nullptr;
     int l1_G = 0;
+    int chance_skip = 0;        // queue a query whose band certainly-ish exceeds K' straight to the
+                                // second chance (no first-pass row reads); needs raw_d
     float* D;
     int64_t* I;
     int* stats;                 // this chunk's device counters (zero on entry): [0] queries left

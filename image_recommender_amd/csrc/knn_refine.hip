@@ -281,6 +281,25 @@ rerank_certify_kernel(const RerankArgs a) {
     const int nvalid = __popcll(__ballot(valid));               // valid candidates come first
     const QueryBounds B(a, q);
 
+    // A query whose K' candidates all sit inside the band this certificate needs (tau - E_a(tau)
+    // at most a quarter bound above the k-th approximate key, tau = min(K'-th candidate, floor))
+    // would pass only if its exact k-th key fell well below the approximate one — observed errors
+    // are ~0.1 of the bound — so it goes to the second chance (a complete procedure of its own)
+    // without the first rerank's row reads (RerankArgs::chance_skip; a wrong guess costs time only)
+    if (a.chance_skip && a.raw_d && nvalid >= kc && k <= kc) {
+        const float a_kk = __shfl(ak, k - 1, 64);
+        float tau0 = __shfl(ak, kc - 1, 64);
+        if (fused) tau0 = fminf(tau0, s_floor);
+        else if (a.floor) tau0 = fminf(tau0, a.floor[q]);
+        if (tau0 - B.bound_a(tau0) <= a_kk + 0.25f * B.bound_a(a_kk)) {
+            if (threadIdx.x == 0) {
+                atomicAdd(a.stats + 2, 1);
+                a.chance_list[atomicAdd(a.stats + 3, 1)] = (int)q;
+            }
+            return;
+        }
+    }
+
     // Only a prefix of the (ascending) candidates can hold the answer; the prefix P = {approx <=
     // prefix_limit(a_k)} is reranked and the first candidate left out bounds every excluded
     // candidate's approximate key from below.

@@ -139,6 +139,7 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
         r.sc_key = ix->sc_key; r.sc_lab = ix->sc_lab; r.sc_meta = ix->sc_meta; r.sc_done = ix->sc_done;
     }
     r.tail_ctl = ix->tail_ctl;
+    r.chance_skip = ix->chance_skip && r.raw_d ? 1 : 0;
     KNN_HIP(launch_rerank_certify(r, st));
     TailArgs t{};
     t.r = r;

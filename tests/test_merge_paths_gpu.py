@@ -6,8 +6,9 @@ batches (RerankArgs::l1_G); the int8 scan's split count depends on the batch siz
 merge route and however many per-split lists the scan writes, the certified top-k is the same rows
 with the same exact fp32 keys (the rerank's key form does not depend on the route), so these
 tests compare the default index against indexes created with IMGREC_MERGE_FUSE=0 (level 2 as its
-own launch) and IMGREC_I8_WGPCU=1 / 5 (256 / 1280 lists per query against the default 512 or
-768: 4 / 20 level-1 groups)
+own launch), IMGREC_I8_WGPCU=1 / 5 (256 / 1280 lists per query against the default 512 or
+768: 4 / 20 level-1 groups) and IMGREC_CHANCE_SKIP=0 (every query through the first rerank, none
+sent straight to the second chance by its band)
 bit for bit, and the default against the float64 oracle (tests/knn_check.py).  The config-2
 distribution (bench.py's 1M x 768 rows) makes most single queries take the second
 chance, so the tail's hand-offs run under every route.
@@ -32,7 +33,7 @@ def corpus(gpu):
     centres = bench.make_centres(torch, cfg, dev, 2)
     blocks = list(bench.gen_rows(torch, cfg, centres, 0, ROWS, dev, 2))
     xb = torch.cat(blocks).cpu().numpy()
-    q = bench.gen_queries(torch, cfg, centres, 32, dev, 2).cpu().numpy()
+    q = bench.gen_queries(torch, cfg, centres, 300, dev, 2).cpu().numpy()
     return xb, q
 
 
@@ -48,20 +49,22 @@ def _index(xb, env, monkeypatch):
 
 
 VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "wgpcu1": {"IMGREC_I8_WGPCU": "1"},
-            "wgpcu5": {"IMGREC_I8_WGPCU": "5"}}
+            "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"}}
 
 
-@pytest.mark.parametrize("nq", [1, 2, 5, 8, 16])
+@pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257])
 def test_routes_return_identical_bits(corpus, monkeypatch, nq):
     """nq 1-8: the int8 path (split counts 1-5 per CU, fused or separate level 2); nq = 16: the
-    bf16 path's small-batch tile with the fused or separate level 2."""
+    bf16 path's small-batch tile with the fused or separate level 2; 256 / 257: the last batch
+    that fuses (one rerank workgroup per CU) and the first that does not.  The float64 oracle
+    checks the default route on up to 16 of the queries."""
     xb, q = corpus
     xq = np.ascontiguousarray(q[:nq])
     base = _index(xb, {}, monkeypatch)
     D0, I0 = base.search(xq, K)
     _, reruns, ratio = base.search_stats(with_error=True)
     assert 0.0 <= ratio < 1.0, ratio
-    check_knn(D0, I0, xb, xq, K, "l2", min_exact_frac=0.5)
+    check_knn(D0[:16], I0[:16], xb, xq[:16], K, "l2", min_exact_frac=0.5)
     for name, env in VARIANTS.items():
         idx = _index(xb, env, monkeypatch)
         D, I = idx.search(xq, K)
