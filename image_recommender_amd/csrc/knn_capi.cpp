@@ -251,7 +251,10 @@ int create_single(int d, int metric, int device, knn_index** out) {
         const int v = std::atoi(e);
         if (v > 0 && v <= 16) ix->i8_wgpcu = v;
     }
-    if (const char* e = std::getenv("IMGREC_MERGE_FUSE")) ix->merge_fuse = *e != '0';
+    if (const char* e = std::getenv("IMGREC_MERGE_FUSE")) {
+        ix->merge_fuse = *e != '0';
+        ix->merge_fuse1 = *e != '0' && *e != '1';
+    }
     if (const char* e = std::getenv("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ix->fence, hipEventDisableTiming) != hipSuccess) {

@@ -21,6 +21,7 @@ __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
 }
 
 constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
+static_assert(kRerankWaves == kRerankWavesHost, "host plans use kRerankWavesHost");
 
 #ifdef IMGREC_TAIL_STAMPS
 // diagnostic build only (tools/tail_stamps.py): s_memrealtime (100 MHz, one clock for every

@@ -41,6 +41,8 @@ struct TileArgs {
 };
 
 // One rerank + certificate launch over merged candidate-pass candidates (knn_refine.hip).
+constexpr int kRerankWavesHost = 8;     // the rerank workgroup's waves (knn_certify.h kRerankWaves)
+
 struct RerankArgs {
     int mode;                   // kModeSplit, kModeBF16 or kModeI8: which error bound certifies
     const float* qp;            // fp32 padded queries, nq x dp
@@ -73,6 +75,10 @@ struct RerankArgs {
     const int64_t* l1_i = nullptr;
     const float* l1_floor = nullptr;
     int l1_G = 0;
+    // l0_lists > 0: the merge's first level fused as well — the raw_lists (= l0_lists <= 64 x
+    // kRerankWaves) per-split lists of 16 are selected by the rerank's waves (one group of 64 lists
+    // a wave, l1_G = groups); no merge launch at all
+    int l0_lists = 0;
     int chance_skip = 0;        // queue a query whose band certainly-ish exceeds K' straight to the
                                 // second chance (no first-pass row reads); needs raw_d
     float* D;

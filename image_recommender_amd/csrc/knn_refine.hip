@@ -230,26 +230,75 @@ rerank_certify_kernel(const RerankArgs a) {
     __shared__ int64_t s_mlab[64];
     __shared__ __attribute__((aligned(16))) uint64_t s_ent[kRerankWaves * 64];
     __shared__ float s_floor;
+    // RerankArgs::l0_lists: the first level too — wave w selects the 16 best of raw lists
+    // 64 w .. 64 w + 63 (wave_select_sorted, as cand_merge_lane_kernel would in its own launch)
+    // into s_ent[16 w ..] and the group's floor (the last key of its full lists) into s_gfl[w]
+    __shared__ uint64_t s_sel[kRerankWaves][64 + 256];
+    __shared__ float s_gfl[kRerankWaves];
     if (fused) {
         constexpr uint64_t kEmpty = ~0ull;
         const int t = threadIdx.x, G = a.l1_G, E = 16 * G;
-        const float* ld = a.l1_d + q * E;
-        const int64_t* li = a.l1_i + q * E;
         uint64_t mine = kEmpty;
-        if (t < E) {
-            const int64_t lb = li[t];
-            if (lb >= 0) mine = ((uint64_t)key_bits_ordered(ld[t]) << 32) | (uint32_t)(lb - id_offset);
-            s_ent[t] = mine;
-        }
-        if (wave == 0) {                                // floor: the level-1 floors and the last
-            float fl = INFINITY;                        // key of every full level-1 list
-            if (lane < G) {
-                fl = a.l1_floor[q * G + lane];
-                if (li[16 * lane + 15] >= 0) fl = fminf(fl, ld[16 * lane + 15]);
-            }
+        if (a.l0_lists > 0) {
+            if (wave < G) {
+                const int l = 64 * wave + lane;
+                const float* rd = a.raw_d + q * a.raw_stride_q + (int64_t)l * 16;
+                const int64_t* ri = a.raw_i + q * a.raw_stride_q + (int64_t)l * 16;
+                uint64_t v[16];
+                float fl = INFINITY;
+                if (l < a.l0_lists) {
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
-            if (lane == 0) s_floor = fl;
+                    for (int p = 0; p < 16; ++p) {
+                        const int64_t lb = ri[p];
+                        v[p] = lb < 0 ? kEmpty
+                                      : ((uint64_t)key_bits_ordered(rd[p]) << 32) | (uint32_t)(lb - id_offset);
+                    }
+                    if (ri[15] >= 0) fl = rd[15];       // a full list: its last key
+                } else {
+#pragma unroll
+                    for (int p = 0; p < 16; ++p) v[p] = kEmpty;
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+                uint64_t m1;
+                int r1;
+                const int K1 = wave_select_sorted<16, 1, 256>(v, 16, s_sel[wave], m1, r1);
+                if (lane < K1) s_ent[16 * wave + r1] = m1;
+                else if (lane < 16) s_ent[16 * wave + lane] = kEmpty;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                // a group that kept 16 bounds the rows it dropped by its 16th key (as level 2
+                // folds a full level-1 list's last key)
+                const uint64_t last = s_ent[16 * wave + 15];
+                if (last != kEmpty) fl = fminf(fl, key_from_ordered((uint32_t)(last >> 32)));
+                if (lane == 0) s_gfl[wave] = fl;
+            }
+            __syncthreads();
+            if (t < E) mine = s_ent[t];
+            if (wave == 0) {
+                float fl = lane < G ? s_gfl[lane] : INFINITY;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+                if (lane == 0) s_floor = fl;
+            }
+        } else {
+            const float* ld = a.l1_d + q * E;
+            const int64_t* li = a.l1_i + q * E;
+            if (t < E) {
+                const int64_t lb = li[t];
+                if (lb >= 0) mine = ((uint64_t)key_bits_ordered(ld[t]) << 32) | (uint32_t)(lb - id_offset);
+                s_ent[t] = mine;
+            }
+            if (wave == 0) {                            // floor: the level-1 floors and the last
+                float fl = INFINITY;                    // key of every full level-1 list
+                if (lane < G) {
+                    fl = a.l1_floor[q * G + lane];
+                    if (li[16 * lane + 15] >= 0) fl = fminf(fl, ld[16 * lane + 15]);
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+                if (lane == 0) s_floor = fl;
+            }
         }
         const int nv = __syncthreads_count(mine != kEmpty);
         const int K = min(kc, nv);
@@ -468,7 +517,10 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;
     if (a.kc > 64 || a.k > a.kc || a.k > 64 || a.dp % 4 != 0 || !a.stats || !a.fail_list)
         return hipErrorInvalidValue;
-    if (a.l1_G > 0 && (16 * a.l1_G > kRerankWaves * 64 || !a.l1_d || !a.l1_i || !a.l1_floor || !a.floor))
+    if (a.l1_G > 0 && (16 * a.l1_G > kRerankWaves * 64 || !a.floor)) return hipErrorInvalidValue;
+    if (a.l1_G > 0 && a.l0_lists == 0 && (!a.l1_d || !a.l1_i || !a.l1_floor)) return hipErrorInvalidValue;
+    if (a.l0_lists > 0 && (a.l1_G != (a.l0_lists + 63) / 64 || a.l1_G > kRerankWaves ||
+                           a.raw_km != 16 || !a.raw_d || !a.raw_i))
         return hipErrorInvalidValue;
     if (a.raw_d && (!a.raw_i || !a.chance_list || a.raw_km < a.k || a.raw_lists <= 0))
         return hipErrorInvalidValue;

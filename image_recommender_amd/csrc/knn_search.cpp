@@ -183,6 +183,14 @@ bool fuse_merge_level2(const knn_index* ix, int64_t nq) {
     return ix->merge_fuse && nq <= ix->cus;
 }
 
+// Both merge levels inside the rerank (RerankArgs::l0_lists): small batches whose merge would
+// take two levels of 16-entry lists with at most one group of 64 lists per rerank wave — no merge
+// launch at all (the level-1 launch was ~9 us of a one-query search).
+bool fuse_merge_level1(const knn_index* ix, int64_t nq, int nlists, int km) {
+    return fuse_merge_level2(ix, nq) && ix->merge_fuse1 && km == 16 && nlists > 64 &&
+           nlists <= 64 * kRerankWavesHost;
+}
+
 // Sibling lockstep of the 256 x 256 bf16 kernel (TileArgs::sync): IMGREC_B16W_SYNC_LAG = the
 // tiles a workgroup may run ahead of the slowest workgroup of its row split; unset or negative =
 // off.
@@ -243,10 +251,13 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
         if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
     }
     int l1G = 0;
-    KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
-                                    ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
-                                    ix->mws_d, ix->mws_i, ix->mws_f, st,
-                                    fuse_merge_level2(ix, nq) ? &l1G : nullptr));
+    const bool l0 = fuse_merge_level1(ix, nq, nlists, km);
+    if (l0) l1G = (nlists + 63) / 64;
+    else
+        KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
+                                        ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
+                                        ix->mws_d, ix->mws_i, ix->mws_f, st,
+                                        fuse_merge_level2(ix, nq) ? &l1G : nullptr));
     RerankArgs r{};
     r.mode = kModeBF16;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
@@ -256,6 +267,7 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
     r.c_trunc = a.ib > 0 ? (float)std::ldexp(1.0, a.ib - 23) : 0.f;
     r.q_resid = ix->q_resid; r.xr_max = ix->xr_max; r.floor = ix->floor;
     if (l1G > 0) { r.l1_d = ix->mws_d; r.l1_i = ix->mws_i; r.l1_floor = ix->mws_f; r.l1_G = l1G; }
+    if (l0) r.l0_lists = nlists;
     r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = km;
     r.raw_stride_q = p.ncand;
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
@@ -295,10 +307,13 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
         if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
     }
     int l1G = 0;
-    KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, p.km, p.ncand, p.km, kc,
-                                    ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
-                                    ix->mws_d, ix->mws_i, ix->mws_f, st,
-                                    fuse_merge_level2(ix, nq) ? &l1G : nullptr));
+    const bool l0 = fuse_merge_level1(ix, nq, nlists, p.km);
+    if (l0) l1G = (nlists + 63) / 64;
+    else
+        KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, p.km, p.ncand, p.km, kc,
+                                        ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
+                                        ix->mws_d, ix->mws_i, ix->mws_f, st,
+                                        fuse_merge_level2(ix, nq) ? &l1G : nullptr));
     RerankArgs r{};
     r.mode = kModeI8;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
@@ -308,6 +323,7 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
     r.c_trunc = 0.f;
     r.q_resid = ix->q8r; r.xr_max = ix->x8r_max; r.floor = ix->floor;
     if (l1G > 0) { r.l1_d = ix->mws_d; r.l1_i = ix->mws_i; r.l1_floor = ix->mws_f; r.l1_G = l1G; }
+    if (l0) r.l0_lists = nlists;
     r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = p.km;
     r.raw_stride_q = p.ncand;
     return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);

@@ -1,12 +1,12 @@
 """The candidate paths' launch knobs must not change a single returned bit.
 
 Round 4 gave the candidate merge two selects (the list-head bound of level 1, the two-entry bound of
-the K' = 64 single level; wave_ops.h) and moved level 2 into the rerank workgroup for small
-batches (RerankArgs::l1_G); the int8 scan's split count depends on the batch size.  Whatever the
+the K' = 64 single level; wave_ops.h) and moved both levels into the rerank workgroup for small
+batches (RerankArgs::l0_lists, l1_G); the int8 scan's split count depends on the batch size.  Whatever the
 merge route and however many per-split lists the scan writes, the certified top-k is the same rows
 with the same exact fp32 keys (the rerank's key form does not depend on the route), so these
-tests compare the default index against indexes created with IMGREC_MERGE_FUSE=0 (level 2 as its
-own launch), IMGREC_I8_WGPCU=1 / 5 (256 / 1280 lists per query against the default 512 or
+tests compare the default index against indexes created with IMGREC_MERGE_FUSE=0 (both levels
+as their own launches) and =1 (level 1 launched, level 2 in the rerank), IMGREC_I8_WGPCU=1 / 5 (256 / 1280 lists per query against the default 512 or
 768: 4 / 20 level-1 groups) and IMGREC_CHANCE_SKIP=0 (every query through the first rerank, none
 sent straight to the second chance by its band)
 bit for bit, and the default against the float64 oracle (tests/knn_check.py).  The config-2
@@ -48,7 +48,8 @@ def _index(xb, env, monkeypatch):
     return idx
 
 
-VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "wgpcu1": {"IMGREC_I8_WGPCU": "1"},
+VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "level2only": {"IMGREC_MERGE_FUSE": "1"},
+            "wgpcu1": {"IMGREC_I8_WGPCU": "1"},
             "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"}}
 
 
