@@ -31,8 +31,14 @@ static_assert(kRerankWaves == kRerankWavesHost, "host plans use kRerankWavesHost
 __device__ unsigned long long g_tail_stamps[1024 * 8];
 #define TAIL_STAMP(slot) do { if (threadIdx.x == 0 && blockIdx.x < 1024) \
     g_tail_stamps[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// the rerank kernel's workgroup 0 (one-query searches): per wave, slots 0 entry, 1 level-1 lists
+// loaded, 2 level-1 selected, 3 level-2 ranked, 4 exit
+__device__ unsigned long long g_rr_stamps[8 * 8];
+#define RR_STAMP(slot) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) \
+    g_rr_stamps[(threadIdx.x >> 6) * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define TAIL_STAMP(slot) do {} while (0)
+#define RR_STAMP(slot) do {} while (0)
 #endif
 
 // Error bounds of one query's certificate (DESIGN.md "bf16 path" / "Split path").

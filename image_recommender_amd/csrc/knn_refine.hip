@@ -207,6 +207,7 @@ rerank_certify_kernel(const RerankArgs a) {
     const int64_t id_offset = a.id_offset;
     // the certificate tail kernel's grid-barrier counters start from zero (it runs next)
     if (a.tail_ctl && blockIdx.x == 0 && threadIdx.x < 4) a.tail_ctl[threadIdx.x] = 0;
+    RR_STAMP(0);
     // exact fp32 keys of the prefix (below): candidate c goes to wave c % kRerankWaves; the query
     // row is loaded first (while wave 0 runs the fused merge level)
     const int n4 = dp / 4;
@@ -260,6 +261,7 @@ rerank_certify_kernel(const RerankArgs a) {
                 }
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+                RR_STAMP(1);
                 uint64_t m1;
                 int r1;
                 const int K1 = wave_select_sorted<16, 1, 256>(v, 16, s_sel[wave], m1, r1);
@@ -272,6 +274,7 @@ rerank_certify_kernel(const RerankArgs a) {
                 const uint64_t last = s_ent[16 * wave + 15];
                 if (last != kEmpty) fl = fminf(fl, key_from_ordered((uint32_t)(last >> 32)));
                 if (lane == 0) s_gfl[wave] = fl;
+                RR_STAMP(2);
             }
             __syncthreads();
             if (t < E) mine = s_ent[t];
@@ -323,6 +326,7 @@ rerank_certify_kernel(const RerankArgs a) {
         }
         if (t == 0) a.floor[q] = s_floor;
         __syncthreads();
+        RR_STAMP(3);
     }
     const int64_t lab = lane < kc ? (fused ? s_mlab[lane] : a.ci[q * kc + lane]) : (int64_t)-1;
     const float ak = lane < kc ? (fused ? s_mkey[lane] : a.cd[q * kc + lane]) : INFINITY;  // ascending
@@ -345,6 +349,7 @@ rerank_certify_kernel(const RerankArgs a) {
                 atomicAdd(a.stats + 2, 1);
                 a.chance_list[atomicAdd(a.stats + 3, 1)] = (int)q;
             }
+            RR_STAMP(4);
             return;
         }
     }
@@ -512,6 +517,12 @@ hipError_t launch_split_rows(const float* src, int64_t n, int dp, int bk, uint32
                        src, n, dp, bk, dst);
     return hipGetLastError();
 }
+
+#ifdef IMGREC_TAIL_STAMPS
+extern "C" int knn_rerank_stamps_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(imgrec::g_rr_stamps), sizeof(imgrec::g_rr_stamps));
+}
+#endif
 
 hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.nq <= 0) return hipSuccess;

@@ -3,8 +3,9 @@
 tailstamps -DIMGREC_TAIL_STAMPS).  Config 2 (1M x 768), int8 path, single queries; for each query
 whose first certificate failed, s_memrealtime (100 MHz, one clock for the whole chip) per tail
 workgroup at: 0 entry, 1 first claim, 2 slice filtered, 3 slice reranked, 4 slice counted,
-5 item merged + answered, 6 plan published / seen, 7 exit.  Prints per-query critical-path
-times in us (relative to the first workgroup's entry) and their medians."""
+5 item merged + answered, 6 plan published / seen, 7 exit; and the rerank workgroup's waves at
+0 entry, 1 level-1 lists loaded, 2 level-1 selected, 3 level-2 ranked, 4 exit (relative to wave 0's
+entry).  Prints per-query critical-path times in us and their medians."""
 import ctypes as C
 import json
 import os
@@ -32,6 +33,7 @@ q = bench.gen_queries(torch, cfg, cent, 32, dev, cid)
 idx = shard.index
 lib = _lib.load()
 buf = (C.c_ulonglong * (1024 * 8))()
+rbuf = (C.c_ulonglong * 64)()
 rows = []
 for i in range(32):
     qi = q[i:i + 1].contiguous()
@@ -44,16 +46,21 @@ for i in range(32):
     if st["second_chance"] == 0:
         continue
     assert lib.knn_tail_stamps_read(buf) == 0
+    assert lib.knn_rerank_stamps_read(rbuf) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8).astype(np.int64)
+    rr = np.frombuffer(rbuf, dtype=np.uint64).reshape(8, 8).astype(np.int64)
     live = a[:, 0] > 0
     t0 = a[live, 0].min()
     us = lambda v: round(float(v - t0) / 100.0, 2)   # 100 MHz ticks -> us
+    r0 = rr[0, 0]
+    rerank = [[round(float(v - r0) / 100.0, 2) if v else None for v in rr[w, :5]] for w in range(8)]
     fin = np.where(a[:, 5] > 0)[0]
     if len(fin) != 1:
         continue
     f = int(fin[0])
     slices = a[a[:, 4] > 0]
-    rec = {"query": i, "wgs": int(live.sum()), "entry_spread_us": us(a[live, 0].max()),
+    rec = {"query": i, "rerank_waves_us": rerank, "rerank_to_tail_us": round(float(t0 - r0) / 100.0, 2),
+           "wgs": int(live.sum()), "entry_spread_us": us(a[live, 0].max()),
            "finisher": [us(v) if v else None for v in a[f]],
            "slice_claim_max_us": us(slices[:, 1].max()), "slice_filtered_max_us": us(slices[:, 2].max()),
            "slice_reranked_max_us": us(slices[:, 3][slices[:, 3] > 0].max()) if (slices[:, 3] > 0).any() else None,
