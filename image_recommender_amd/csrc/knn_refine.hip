@@ -220,6 +220,10 @@ rerank_certify_kernel(const RerankArgs a) {
             qr[it] = i < n4 ? q4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
+#ifdef IMGREC_TAIL_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // (diagnostic: the query row's round trip)
+    RR_STAMP(5);
+#endif
     // the candidate merge's second level (RerankArgs::l1_G): the query's E = 16 l1_G level-1
     // entries (<= one per thread) packed (order-preserving key bits | row) in LDS; each thread
     // ranks its entry against all E (broadcast LDS reads; entries are distinct: a row sits in
@@ -262,6 +266,20 @@ rerank_certify_kernel(const RerankArgs a) {
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
                 RR_STAMP(1);
+#ifdef IMGREC_TAIL_STAMPS
+                {   // diagnostic: the same lists loaded again (warm caches, warm code): slot 6
+                    const int l2_ = 64 * wave + lane;
+                    const float* rd2 = a.raw_d + q * a.raw_stride_q + (int64_t)l2_ * 16;
+                    const int64_t* ri2 = a.raw_i + q * a.raw_stride_q + (int64_t)l2_ * 16;
+                    uint64_t acc2 = 0;
+                    if (l2_ < a.l0_lists) {
+#pragma unroll
+                        for (int p = 0; p < 16; ++p) acc2 += (uint64_t)ri2[p] ^ __float_as_uint(rd2[p]);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" :: "v"(acc2) : "memory");
+                    RR_STAMP(6);
+                }
+#endif
                 uint64_t m1;
                 int r1;
                 const int K1 = wave_select_sorted<16, 1, 256>(v, 16, s_sel[wave], m1, r1);

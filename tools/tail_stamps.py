@@ -4,8 +4,8 @@ tailstamps -DIMGREC_TAIL_STAMPS).  Config 2 (1M x 768), int8 path, single querie
 whose first certificate failed, s_memrealtime (100 MHz, one clock for the whole chip) per tail
 workgroup at: 0 entry, 1 first claim, 2 slice filtered, 3 slice reranked, 4 slice counted,
 5 item merged + answered, 6 plan published / seen, 7 exit; and the rerank workgroup's waves at
-0 entry, 1 level-1 lists loaded, 2 level-1 selected, 3 level-2 ranked, 4 exit (relative to wave 0's
-entry).  Prints per-query critical-path times in us and their medians."""
+0 entry, 1 level-1 lists loaded, 2 level-1 selected, 3 level-2 ranked, 4 exit, 5 query row loaded, 6 the
+same lists loaded a second time (relative to wave 0's entry).  Prints per-query critical-path times in us and their medians."""
 import ctypes as C
 import json
 import os
@@ -53,7 +53,7 @@ for i in range(32):
     t0 = a[live, 0].min()
     us = lambda v: round(float(v - t0) / 100.0, 2)   # 100 MHz ticks -> us
     r0 = rr[0, 0]
-    rerank = [[round(float(v - r0) / 100.0, 2) if v else None for v in rr[w, :5]] for w in range(8)]
+    rerank = [[round(float(v - r0) / 100.0, 2) if v else None for v in rr[w, :7]] for w in range(8)]
     fin = np.where(a[:, 5] > 0)[0]
     if len(fin) != 1:
         continue
