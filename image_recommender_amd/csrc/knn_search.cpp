@@ -139,7 +139,10 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
         r.sc_key = ix->sc_key; r.sc_lab = ix->sc_lab; r.sc_meta = ix->sc_meta; r.sc_done = ix->sc_done;
     }
     r.tail_ctl = ix->tail_ctl;
-    r.chance_skip = ix->chance_skip && r.raw_d ? 1 : 0;
+    // (small batches only: a large batch's rerank is throughput-bound and its second chances
+    // queue up in the tail; at 1024 queries the A/B was within the +-15 us noise of the step,
+    // profiles/r04/chance_skip/ab_env_nq1024*.txt, so large batches keep the round-3 route)
+    r.chance_skip = ix->chance_skip && r.raw_d && nq <= ix->cus ? 1 : 0;
     KNN_HIP(launch_rerank_certify(r, st));
     TailArgs t{};
     t.r = r;
