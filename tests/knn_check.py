@@ -10,8 +10,9 @@ Contract: for every query row
 
 check_knn_tight adds the integer-exact label claim of north_star at an EMPIRICAL tie window
 (VERDICT r03 item 1): the window is a stated multiple of the largest |fp32 key - float64 key|
-actually measured over the returned pairs (this build's and, when given, the faiss-restated fp32
-oracle's), about 1e-6 of the key scale instead of the rigorous ~1e-4.  At every rank separated from
+measured on the faiss-restated fp32 oracle's returned pairs (this build's own when that oracle is
+not run: cosine / IP, or corpora past BLAS_MAX_WORK), about 1e-6 of the key scale instead of the
+rigorous ~1e-4; the build's own error is asserted below BUILD_ERR_REL_MAX of the key scale.  At every rank separated from
 its neighbours by more than that window the labels must equal the float64 oracle's AND the
 faiss-restated fp32 oracle's (oracle.flat_knn.search_blas_fp32_blocked = faiss's
 exhaustive_L2sqr_blas), and the top-k label SET must equal both wherever the k-th / (k+1)-th
@@ -23,6 +24,7 @@ from oracle.flat_knn import fp32_error_bound, search_exact
 
 WINDOW_MULT = 8.0        # empirical window = WINDOW_MULT x the measured max |fp32 - float64|
 WINDOW_REL_FLOOR = 1e-6  # ... and at least this fraction of the query's key scale
+BUILD_ERR_REL_MAX = 1e-5  # the build's own max |fp32 key - float64| stays below this x key scale
 
 
 def _pair_bound(xb, xq, qi, ids, metric):
@@ -132,14 +134,24 @@ def _tight_labels(D, I, xb, xq, k, metric, oracle, blas, min_rank_frac, min_set_
         Db, Ib = np.asarray(blas[0], np.float64), np.asarray(blas[1])
         exb = np.stack([_exact_pair(xb, xq, q, Ib[q, :nv], metric) for q in range(nq)])
         err_blas = float(np.abs(exb - Db[:, :nv]).max())
-    E = max(err, err_blas)
+    # The window comes from the oracle side wherever it can: the faiss-restated fp32
+    # error when that restatement ran, so a build whose returned keys regress cannot widen the
+    # window its own labels are checked at.  The build's own error is held separately below a
+    # fixed fraction of the key scale.
+    E = err_blas if blas is not None else err
+    scales = np.array([float(np.abs(Dg[q, :nv + 1][Ig[q, :nv + 1] >= 0]).max()) for q in range(nq)])
+    key_scale = float(scales.max()) if nq else 0.0
+    assert err <= BUILD_ERR_REL_MAX * key_scale + 1e-30, \
+        (tag, "build's |fp32 key - float64| above the stated fraction of the key scale", err, key_scale)
     rank_ok = rank_tot = set_ok = set_tot = 0
     worst_rel = 0.0
     for q in range(nq):
         gd = Dg[q]
-        scale = float(np.abs(gd[:nv + 1][Ig[q, :nv + 1] >= 0]).max())
+        scale = scales[q]
         w = max(WINDOW_MULT * E, WINDOW_REL_FLOOR * scale)
-        if scale > 0:                      # (a query whose answers all sit at distance 0: no scale)
+        # (the printed ratio skips queries whose answers sit at distance ~0 — e.g. a query equal to
+        # a stored row under L2 — where the key scale is rounding noise, not a scale)
+        if scale > WINDOW_MULT * max(E, 1e-30):
             worst_rel = max(worst_rel, w / scale)
         for j in range(nv):
             rank_tot += 1

@@ -60,3 +60,18 @@ def test_cpu_comparator_is_exact_flat_search():
     assert (I == Ig).mean() > 0.99           # fp32 near-ties may swap
     np.testing.assert_allclose(D, Dg, rtol=0, atol=1e-4)
     assert (np.diff(D, axis=1) >= 0).all()
+
+
+def test_cpu_comparator_single_query_leg():
+    """bench.py's nq = 1 CPU leg (the reference CLI's regime): the same port with the row norms
+    precomputed, one query against every row, returns the float64 oracle's neighbours."""
+    import numpy as np
+    from oracle.flat_knn import search_blas_fp32_blocked, search_exact
+    from tests.datagen import concat_rows
+    xb = concat_rows(20000, seed=13)
+    xq = concat_rows(3, seed=14)
+    xn = (xb * xb).sum(1, dtype=np.float32)
+    for i in range(3):
+        D, I = search_blas_fp32_blocked(xb, xq[i:i + 1], 10, block=4096, threads=4, xb_norms=xn)
+        Dg, Ig = search_exact(xb, xq[i:i + 1], 10, "l2")
+        assert (I == Ig).mean() > 0.9 and np.allclose(D, Dg, rtol=0, atol=1e-5)

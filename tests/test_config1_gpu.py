@@ -1,9 +1,21 @@
-"""SURVEY §8(d) config 1 as a parity case: N = 10,000 rows of D = 512 in the `dreamsim_vectors`
-table (pickled float32 BLOBs, vector_scripts/create_vector_base.py:144), built by the drop-in
-FAISSIndexBuilderDB (main/create_index.py:251-325) and searched through ImageRecommender
-(main/search_from_image.py:194-254) with 100 self-queries served from the DB cache
-(images_root='.', `_plot_results` stubbed).  Every result list is checked against the float64
-oracle on the normalised query (main/search_from_image.py:322).
+"""The reference CLI path held to the integer-exact label claim.
+
+SURVEY §8(d) config 1: N = 10,000 rows of D = 512 in the `dreamsim_vectors` table (pickled
+float32 BLOBs, vector_scripts/create_vector_base.py:144), built by the drop-in FAISSIndexBuilderDB
+(main/create_index.py:251-325) and searched through ImageRecommender
+(main/search_from_image.py:219-254) with 100 self-queries served from the DB cache
+(images_root='.', `_plot_results` stubbed).
+
+A second case runs the reference's default feature combination: a 20,000-row three-part DB
+(color 48 | sift 128 | dreamsim 1792 BLOBs, each part unit-norm as the extractors store them)
+built through create_index with vector_types color,sift,dreamsim, searched with single images and
+with two-image averaged queries (main/search_from_image.py:275-324: concat, mean, normalize_L2).
+Every CLI call is one query (nq = 1: the int8 candidate route).
+
+The vector each call actually searched is captured from `_extract_query_vector`; the 100 result
+lists are then checked with `check_knn_tight` against float64 AND the faiss-restated fp32 oracle
+(oracle.flat_knn.search_blas_fp32_blocked) at the empirical window, with at least 95 % of the
+ranks and 90 % of the top-k sets checked label for label.
 """
 import pickle
 import sqlite3
@@ -12,53 +24,108 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from oracle.flat_knn import fp32_error_bound, search_exact
+from oracle.flat_knn import search_blas_fp32_blocked, search_exact
+from tests.datagen import concat_rows
+from tests.knn_check import check_knn_tight
 
 pytestmark = pytest.mark.gpu
 
-N, D, K = 10_000, 512, 10
+K = 10
 
 
-def _make_db(path: Path) -> np.ndarray:
+def _make_db(path: Path, tables: dict, n: int, folder: str) -> None:
     from image_recommender_amd.main.create_db import create_schema
-    rng = np.random.default_rng(0)
-    centres = rng.standard_normal((200, D))
-    x = (centres[rng.integers(0, 200, N)] + 0.5 * rng.standard_normal((N, D))).astype(np.float32)
     con = sqlite3.connect(path)
     create_schema(con)
     con.executemany("INSERT INTO images (path) VALUES (?)",
-                    [(f"image_data/c1/{i:05d}.png",) for i in range(N)])
-    con.executemany("INSERT INTO dreamsim_vectors (image_id, dreamsim_vector_blob) VALUES (?, ?)",
-                    [(i + 1, pickle.dumps(x[i], protocol=5)) for i in range(N)])
+                    [(f"image_data/{folder}/{i:05d}.png",) for i in range(n)])
+    for vt, mat in tables.items():
+        con.executemany(f"INSERT INTO {vt}_vectors (image_id, {vt}_vector_blob) VALUES (?, ?)",
+                        [(i + 1, pickle.dumps(mat[i], protocol=5)) for i in range(n)])
     con.commit()
     con.close()
-    return x
+
+
+def _cli_run(tmp_path, vector_types, index_type, folder, queries):
+    """Build through FAISSIndexBuilderDB, then one ImageRecommender call per query (a list of
+    image numbers).  Returns (D, I, Q, paths): the distances / offsets of the K results, the
+    float32 query row each call searched, and the search paths the library took."""
+    from image_recommender_amd import _lib
+    from image_recommender_amd.main.create_index import FAISSIndexBuilderDB
+    from image_recommender_amd.main.search_from_image import ImageRecommender
+    idx = FAISSIndexBuilderDB(db_path="images.db", vector_types=vector_types,
+                              log_dir=str(tmp_path / "logs")).build_index()
+    assert idx is not None
+    rec = ImageRecommender(images_root=".", db_path=str(tmp_path / "images.db"), top_k=K)
+    rec._plot_results = lambda *a, **k: None
+    seen = []
+    extract = rec._extract_query_vector
+
+    def capture(*a, **kw):
+        v = extract(*a, **kw)
+        seen.append(None if v is None else np.array(v, dtype=np.float32).reshape(-1))
+        return v
+    rec._extract_query_vector = capture
+    D = np.full((len(queries), K), np.inf)
+    I = np.full((len(queries), K), -1, np.int64)
+    paths = []
+    for j, imgs in enumerate(queries):
+        res = rec.search_similar_images(
+            [str(tmp_path / f"image_data/{folder}/{i:05d}.png") for i in imgs], index_type)
+        assert res is not None and len(res) == K, (j, imgs)
+        # offsets are dense ranks of image_id among complete rows: image i (id i + 1) -> offset i
+        I[j] = [int(Path(p).stem) for p, _ in res]
+        D[j] = [d for _, d in res]
+        index = rec._indexes[next(iter(rec._indexes))][0]
+        paths.append(_lib.load().knn_last_path(index.handle))
+    Q = np.stack(seen)
+    assert Q.shape == (len(queries), idx.d) and np.isfinite(Q).all()
+    return D, I, Q, paths
+
+
+def _check(D, I, x, Q, tag):
+    oracle = search_exact(x, Q, K + 1, "l2")
+    blas = search_blas_fp32_blocked(x, Q, K, threads=8)
+    return check_knn_tight(D, I, x, Q, K, "l2", oracle=oracle, blas=blas, min_rank_frac=0.95,
+                           min_set_frac=0.9, tag=tag)
 
 
 def test_config1_build_and_cli_search(gpu, tmp_path, monkeypatch):
     monkeypatch.chdir(tmp_path)
-    x = _make_db(tmp_path / "images.db")
-    from image_recommender_amd.main.create_index import FAISSIndexBuilderDB
-    from image_recommender_amd.main.search_from_image import ImageRecommender
-    idx = FAISSIndexBuilderDB(db_path="images.db", vector_types=["dreamsim"],
-                              log_dir=str(tmp_path / "logs")).build_index()
-    assert idx.ntotal == N and idx.d == D
-    rec = ImageRecommender(images_root=".", db_path=str(tmp_path / "images.db"), top_k=K)
-    rec._plot_results = lambda *a, **k: None
-    qids = np.random.default_rng(1).choice(N, 100, replace=False)
-    q = x[qids].astype(np.float64)
-    q = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
-    Dg, Ig = search_exact(x, q, K, "l2")
-    for j, i in enumerate(qids):
-        res = rec.search_similar_images([str(tmp_path / f"image_data/c1/{i:05d}.png")], "dreamsim")
-        assert res is not None and len(res) == K
-        got_ids = [int(Path(p).stem) for p, _ in res]
-        got_d = np.array([d for _, d in res])
-        tol = fp32_error_bound(x[got_ids], q[j][None, :], "l2")[0] * 1.0001 + 1e-30
-        np.testing.assert_array_less(np.abs(got_d - Dg[j]), tol + 1e-7)
-        # (no "self match first": the query is normalised but rows are not, SURVEY Appendix C.4,
-        # so a same-cluster row of smaller norm can rank before the query's own row)
-        # identical ranking up to exact-tie windows
-        for r, (gi, wi) in enumerate(zip(got_ids, Ig[j])):
-            if gi != wi:
-                assert abs(Dg[j][r] - np.sum((x[gi].astype(np.float64) - q[j]) ** 2)) <= 2 * tol[r]
+    n, d = 10_000, 512
+    rng = np.random.default_rng(0)
+    centres = rng.standard_normal((200, d))
+    x = (centres[rng.integers(0, 200, n)] + 0.5 * rng.standard_normal((n, d))).astype(np.float32)
+    _make_db(tmp_path / "images.db", {"dreamsim": x}, n, "c1")
+    qids = np.random.default_rng(1).choice(n, 100, replace=False)
+    D, I, Q, paths = _cli_run(tmp_path, ["dreamsim"], "dreamsim", "c1", [[int(i)] for i in qids])
+    # the searched vector is the stored row, normalised (main/search_from_image.py:322)
+    ref = x[qids].astype(np.float64)
+    ref /= np.linalg.norm(ref, axis=1, keepdims=True)
+    assert np.abs(Q - ref).max() < 1e-6
+    res = _check(D, I, x, Q, "config1 CLI 10k x 512")
+    print(f"[config1 CLI] search paths taken: {sorted(set(paths))} (3 = int8, 2 = bf16); {res}")
+
+
+def test_three_part_cli_single_and_averaged_queries(gpu, tmp_path, monkeypatch):
+    """20k x 1968 color|sift|dreamsim, the reference's default combination, built in caller order
+    color,sift,dreamsim (the search resolves the build order from the index metadata, SURVEY
+    Appendix C.1); 60 single-image and 40 two-image averaged CLI queries."""
+    monkeypatch.chdir(tmp_path)
+    n = 20_000
+    x = concat_rows(n, seed=11)
+    parts = {"color": x[:, :48], "sift": x[:, 48:176], "dreamsim": x[:, 176:]}
+    _make_db(tmp_path / "images.db", {k: np.ascontiguousarray(v) for k, v in parts.items()}, n, "c3")
+    rng = np.random.default_rng(2)
+    singles = [[int(i)] for i in rng.choice(n, 60, replace=False)]
+    pairs = [[int(a), int(b)] for a, b in rng.choice(n, (40, 2), replace=False)]
+    D, I, Q, paths = _cli_run(tmp_path, ["color", "sift", "dreamsim"], "color,sift,dreamsim", "c3",
+                              singles + pairs)
+    # averaged queries: the mean of the two stored rows in build order, then normalize_L2
+    for j, imgs in enumerate(singles + pairs):
+        ref = x[imgs].astype(np.float64).mean(0)
+        ref /= np.linalg.norm(ref)
+        assert np.abs(Q[j] - ref).max() < 1e-6, j
+    assert all(p == 3 for p in paths), paths          # nq = 1 on the int8 candidate route
+    res = _check(D, I, x, Q, "three-part CLI 20k x 1968")
+    print(f"[three-part CLI] {res}")
