@@ -14,6 +14,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <string>
 
 #include "knn_index.h"
 #include "knn_multi.h"
@@ -23,6 +25,26 @@ namespace imgrec {
 namespace {
 thread_local std::string g_err;
 }  // namespace
+
+// The A/B and test knobs read at index creation (IMGREC_CUS, IMGREC_I8_WGPCU, IMGREC_MERGE_FUSE,
+// IMGREC_CHANCE_SKIP, IMGREC_B16W_SYNC_LAG; INTEGRATION.md "A/B switches"): not product settings.
+// An inherited one silently re-plans every launch, so the first read of each that is set says so
+// once on stderr.
+const char* test_knob(const char* name) {
+    const char* e = std::getenv(name);
+    if (e && *e) {
+        static std::mutex mu;
+        static std::string seen;
+        std::lock_guard<std::mutex> lk(mu);
+        const std::string tag = std::string("|") + name + "|";
+        if (seen.find(tag) == std::string::npos) {
+            seen += tag;
+            std::fprintf(stderr, "[imgrec] %s=%s overrides a launch default (test / A-B knob, "
+                                 "INTEGRATION.md)\n", name, e);
+        }
+    }
+    return e && *e ? e : nullptr;
+}
 
 void set_err(const char* fmt, ...) {
     char buf[512];
@@ -43,8 +65,10 @@ const char* last_error() { return g_err.c_str(); }
 // only when a different stream arrives: back-to-back operations on one stream then pay no event
 // record (each costs ~5.7 us of idle GPU between the kernels around it on MI355X,
 // profiles/r03/), but the remembered stream must stay valid until that next operation, and the
-// wait covers whatever the caller queued on it meanwhile.  A lazy record that fails (a destroyed
-// stream) falls back to a device-wide synchronisation instead of wedging the index.
+// wait covers whatever the caller queued on it meanwhile.  A lazy record that reports an error
+// falls back to a device-wide synchronisation instead of wedging the index — best effort only:
+// recording on a stream the caller has destroyed is a use after free, not a guaranteed error
+// return, so in lazy mode the stream MUST outlive the next call on the index (imgrec_knn.h).
 // Host-pointer operations synchronise their stream before returning and leave no fence.
 int fence_begin(knn_index* ix, hipStream_t st) {
     if (!ix->fence_set || ix->fence_stream == st) return KNN_OK;
@@ -243,19 +267,19 @@ int create_single(int d, int metric, int device, knn_index** out) {
         cus > 0)
         ix->cus = cus;
     // IMGREC_CUS=n (tests): plan launches for n CUs, as on a partitioned device (CPX mode)
-    if (const char* e = std::getenv("IMGREC_CUS")) {
+    if (const char* e = test_knob("IMGREC_CUS")) {
         const int v = std::atoi(e);
         if (v > 0 && v < ix->cus) ix->cus = v;
     }
-    if (const char* e = std::getenv("IMGREC_I8_WGPCU")) {
+    if (const char* e = test_knob("IMGREC_I8_WGPCU")) {
         const int v = std::atoi(e);
         if (v > 0 && v <= 16) ix->i8_wgpcu = v;
     }
-    if (const char* e = std::getenv("IMGREC_MERGE_FUSE")) {
+    if (const char* e = test_knob("IMGREC_MERGE_FUSE")) {
         ix->merge_fuse = *e != '0';
         ix->merge_fuse1 = *e != '0' && *e != '1';
     }
-    if (const char* e = std::getenv("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
+    if (const char* e = test_knob("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ix->fence, hipEventDisableTiming) != hipSuccess) {
         if (ix->stream) (void)hipStreamDestroy(ix->stream);

@@ -18,6 +18,8 @@
 namespace imgrec {
 
 void set_err(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+// the value of a test / A-B environment knob, logged once on stderr when set (knn_capi.cpp)
+const char* test_knob(const char* name);
 
 #define KNN_FAIL(code, ...)              \
     do {                                 \

@@ -199,7 +199,7 @@ bool fuse_merge_level1(const knn_index* ix, int64_t nq, int nlists, int km) {
 // off.
 int b16_sync_lag() {
     static const int v = [] {
-        const char* e = std::getenv("IMGREC_B16W_SYNC_LAG");
+        const char* e = test_knob("IMGREC_B16W_SYNC_LAG");
         return e && *e ? std::atoi(e) : -1;
     }();
     return v;

@@ -127,7 +127,8 @@ def _hlin(m, x, act="none"):
     n, k = w.shape
     if k % 64 or n % 256 or x.dtype != torch.bfloat16:
         y = _lin(m, x)
-        return {"none": lambda t: t, "gelu": _gelu_, "quick_gelu": _quick_gelu_}[act](y.contiguous())
+        return {"none": lambda t: t, "gelu": _gelu_, "quick_gelu": _quick_gelu_,
+                "gelu_tanh": _gelu_tanh}[act](y.contiguous())
     x = x.contiguous()
     y = torch.empty((*x.shape[:-1], n), dtype=torch.bfloat16, device=x.device)
     b = getattr(m, "b_f32", None)
@@ -214,6 +215,13 @@ def _gelu_(h):
     if rc != 0:
         raise RuntimeError("vit_gelu_bf16 failed")
     return h
+
+
+def _gelu_tanh(h):
+    """GELU's tanh form on a bf16 tensor, evaluated in fp32 (the fallback of _hlin's fused
+    "gelu_tanh" epilogue for shapes vit_linear_bf16 does not take)."""
+    import torch
+    return torch.nn.functional.gelu(h.float(), approximate="tanh").to(torch.bfloat16)
 
 
 def _quick_gelu_(h):

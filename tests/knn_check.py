@@ -12,7 +12,7 @@ check_knn_tight adds the integer-exact label claim of north_star at an EMPIRICAL
 (VERDICT r03 item 1): the window is a stated multiple of the largest |fp32 key - float64 key|
 measured on the faiss-restated fp32 oracle's returned pairs (this build's own when that oracle is
 not run: cosine / IP, or corpora past BLAS_MAX_WORK), about 1e-6 of the key scale instead of the
-rigorous ~1e-4; the build's own error is asserted below BUILD_ERR_REL_MAX of the key scale.  At every rank separated from
+rigorous ~1e-4; the build's own error is asserted below BUILD_ERR_REL_MAX of |q|^2 + |x|^2.  At every rank separated from
 its neighbours by more than that window the labels must equal the float64 oracle's AND the
 faiss-restated fp32 oracle's (oracle.flat_knn.search_blas_fp32_blocked = faiss's
 exhaustive_L2sqr_blas), and the top-k label SET must equal both wherever the k-th / (k+1)-th
@@ -24,7 +24,7 @@ from oracle.flat_knn import fp32_error_bound, search_exact
 
 WINDOW_MULT = 8.0        # empirical window = WINDOW_MULT x the measured max |fp32 - float64|
 WINDOW_REL_FLOOR = 1e-6  # ... and at least this fraction of the query's key scale
-BUILD_ERR_REL_MAX = 1e-5  # the build's own max |fp32 key - float64| stays below this x key scale
+BUILD_ERR_REL_MAX = 1e-5  # the build's own max |fp32 key - float64| stays below this x (|q|^2 + |x|^2)
 
 
 def _pair_bound(xb, xq, qi, ids, metric):
@@ -137,12 +137,17 @@ def _tight_labels(D, I, xb, xq, k, metric, oracle, blas, min_rank_frac, min_set_
     # The window comes from the oracle side wherever it can: the faiss-restated fp32
     # error when that restatement ran, so a build whose returned keys regress cannot widen the
     # window its own labels are checked at.  The build's own error is held separately below a
-    # fixed fraction of the key scale.
+    # fixed fraction of the scale of the key's terms.
     E = err_blas if blas is not None else err
     scales = np.array([float(np.abs(Dg[q, :nv + 1][Ig[q, :nv + 1] >= 0]).max()) for q in range(nq)])
-    key_scale = float(scales.max()) if nq else 0.0
-    assert err <= BUILD_ERR_REL_MAX * key_scale + 1e-30, \
-        (tag, "build's |fp32 key - float64| above the stated fraction of the key scale", err, key_scale)
+    # the scale of the terms the fp32 key is formed from: |q|^2 + |x|^2 (L2; a near-duplicate's key
+    # is a cancellation far below it), |q| |x| (inner products)
+    qn = (xq.astype(np.float64) ** 2).sum(1)
+    xn = (xb[np.unique(np.where(I[:, :nv] < 0, 0, I[:, :nv]))].astype(np.float64) ** 2).sum(1).max()
+    term_scale = float((qn + xn).max() if metric == "l2"
+                       else (1.0 if metric == "cosine" else np.sqrt(qn.max() * xn)))
+    assert err <= BUILD_ERR_REL_MAX * term_scale + 1e-30, \
+        (tag, "build's |fp32 key - float64| above the stated fraction of |q|^2 + |x|^2", err, term_scale)
     rank_ok = rank_tot = set_ok = set_tot = 0
     worst_rel = 0.0
     for q in range(nq):

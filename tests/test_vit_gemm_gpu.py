@@ -83,6 +83,15 @@ def test_linear_without_bias_and_refusals(gpu):
                                256, 0, C.c_void_p(out.data_ptr()), None) == -1
     y2, ref2, absum2 = _linear(10, 96, 200, seed=4, bf16_bias=True)   # k % 64, n % 256: _lin path
     _within(y2, ref2, absum2)
+    # fc1's fused activation on a fallback shape: _lin, then the activation in fp32
+    # on the bf16-rounded pre-activation; stated bound: that rounding (2^-9 |pre|) through the
+    # activation's slope (< 1.13 for GELU) plus the output's own bf16 rounding
+    for act in ("gelu_tanh", "gelu", "quick_gelu"):
+        y3, ref3, absum3 = _linear(10, 96, 200, act, seed=5, bf16_bias=True)
+        pre = _linear(10, 96, 200, "none", seed=5, bf16_bias=True)[1]
+        err = (y3.float() - ref3).abs()
+        bound = ref3.abs() * 2.0 ** -8 + pre.abs() * 1.2 * 2.0 ** -8 + absum3 * 2.0 ** -20 + 1e-30
+        assert float((err / bound).max()) <= 1.0, act
 
 
 def test_forward_on_hip_gemm_matches_hipblaslt(gpu):
