@@ -24,7 +24,8 @@
 #                   -DIMGREC_B16_STAMPS)
 #   tailstamps=CFG  tools/tail_stamps.py: certificate-tail workgroup timestamps of one-query second
 #                   chances (lib/libimgrec_tailstamps.so: build_variants.sh tailstamps -DIMGREC_TAIL_STAMPS)
-#   ab=LIB          A/B of lib/libimgrec.so and lib/LIB: per-step and kernel ms on cfg2 and cfg3
+#   ab=LIB          A/B of lib/libimgrec.so and lib/LIB: per-step and kernel ms on cfg2, cfg3 and
+#                   the 125k-row shard
 #                   (profile-only, twice alternating) -> ab_LIB.txt
 # Extra bench arguments for every bench stage: BENCH_ARGS.
 set -u
@@ -108,8 +109,9 @@ for st in "$@"; do
     ab)
       for rep in 1 2; do
         for lib in libimgrec.so $arg; do
-          for c in 2 3; do
-            IMGREC_LIB_NAME=$lib timeout -k 10 200 python bench.py --config $c --profile-only --steps 60 --warmup 20 \
+          for c in 2 3 r125k; do
+            ca="--config $c"; [ $c = r125k ] && ca="--rows 125000"
+            IMGREC_LIB_NAME=$lib timeout -k 10 200 python bench.py $ca --profile-only --no-phases --steps 60 --warmup 20 \
               > $OUT/ab.json 2>> $OUT/ab.err || fail ab $OUT/ab.err
             python3 -c "import json;d=json.load(open('$OUT/ab.json'));print('$rep $lib cfg$c step', round(d['ms_per_step'],4), 'kernel', round(d['kernel_ms'],4))" | tee -a $OUT/ab_$arg.txt
           done
