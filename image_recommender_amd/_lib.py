@@ -65,6 +65,7 @@ SIGNATURES = {
     "knn_search_stats": (_i, [_vp, _pi64, _pi64, _pf]),
     "knn_search_stats2": (_i, [_vp, _pi64, _pi64, _pi64, _pf]),
     "knn_last_path": (_i, [_vp]),
+    "knn_large_k_fallbacks": (_i, [_vp, C.POINTER(_i64)]),
     "knn_last_error": (C.c_char_p, []),
     "knn_version": (C.c_char_p, []),
     # imgrec_color.h

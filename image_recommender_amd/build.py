@@ -75,7 +75,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = True) -> Path:
     if force or _stale(LIB, objs):
         tmp = LIB.with_suffix(".so.tmp")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + \
-              [str(o) for o in objs] + ["-lrocblas"]
+              [str(o) for o in objs]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

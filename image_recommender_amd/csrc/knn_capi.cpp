@@ -650,6 +650,17 @@ int knn_last_path(const knn_index_t* ix) {
     return ix->multi ? multi_last_path(ix) : ix->last_path;
 }
 
+int knn_large_k_fallbacks(const knn_index_t* ix, int64_t* n) {
+    if (!ix || !n) KNN_FAIL(KNN_EINVAL, "NULL argument");
+    if (!ix->multi) {
+        *n = ix->lk_last_fallbacks;
+        return KNN_OK;
+    }
+    *n = 0;
+    for (int s = 0; s < multi_num_shards(ix); ++s) *n += multi_shard(ix, s)->lk_last_fallbacks;
+    return KNN_OK;
+}
+
 int knn_plan(const knn_index_t* cix, int64_t nq, int k, int* tr, int* tq, int* splits, int* wgs) {
     if (!cix || !tr || !tq || !splits || !wgs) KNN_FAIL(KNN_EINVAL, "NULL argument");
     const knn_index* ix = cix->multi ? multi_shard(cix, 0) : cix;

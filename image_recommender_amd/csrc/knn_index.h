@@ -183,10 +183,10 @@ struct knn_index {
     size_t ev_used = 0;
     // one index over several devices (knn_multi.cpp); NULL for a single-device index
     struct knn_multi* multi = nullptr;
-    // k > KNN_MAX_K (knn_largek.hip): rocBLAS handle, GEMM block, running top-k lists
-    void* blas = nullptr;
-    float* lk_g = nullptr; size_t lk_g_cap = 0;
+    // k > KNN_MAX_K (knn_largek.hip): the fallback's stripe lists, the uncertified queries (+ count)
     uint64_t* lk_run = nullptr; size_t lk_run_cap = 0;
+    int* lk_fail = nullptr; size_t lk_fail_cap = 0;
+    int64_t lk_last_fallbacks = 0;   // queries the large-k certificate sent to the exact scan (total)
 };
 
 namespace imgrec {

@@ -1,22 +1,29 @@
-// knn_largek.hip — exact search for KNN_MAX_K < k <= KNN_MAX_K_LARGE (gfx950).
+// knn_largek.hip — exact search for KNN_MAX_K < k <= KNN_MAX_K_LARGE (gfx950), hand-written
+// end to end (no vendor GEMM, no N x Q key block in HBM).
 //
 // The fused kernels keep register top-k lists (k <= 32).  faiss IndexFlat serves any k
-// (main/search_from_image.py:247 passes the CLI's --top-k), so larger k runs faiss's own flat
-// algorithm instead (exhaustive_L2sqr_blas): an fp32 GEMM of a query block against a corpus
-// block (rocBLAS sgemm, alpha = -2: G = -2 q.x exactly), keys formed with the stored norms in the
-// same (|q|^2 + |x|^2) - 2 q.x form as every other path, and per query a running top-k merged
-// with each block by an exact radix select in LDS:
-//   * a workgroup per query packs the block's keys with their rows into u64 (order-preserving
-//     key bits | row: unsigned order = (key, row), faiss's tie rule) next to the running list;
-//   * eight 8-bit digit passes of a 256-bin LDS histogram find the k-th smallest value T;
-//   * the values < T, then copies of T, fill the new running list (empties = ~0 pad a corpus
-//     with fewer than k rows); after the last block a bitonic sort orders it and the workgroup
-//     writes D / I.
-// Throughput is the GEMM's (the selection reads the block from L2); this path exists for
-// completeness of the faiss surface, the k <= 32 paths are the fast ones.
+// (main/search_from_image.py:247 passes the CLI's --top-k), so larger k runs in three steps:
+//   1. the exact fp32 tile kernel (knn_tile_topk_kernel, KM = 32) over the whole corpus: per
+//      (query, row split, list) the 32 best (key, row) of that list's rows — the key in the same
+//      (|q|^2 + |x|^2) - 2 q.x form as every other path;
+//   2. largek_union_kernel, a workgroup per query: the k best of the union of all lists by an
+//      exact radix select in LDS (running top-k over chunks of the lists), certified against the
+//      lists' FLOOR: a row no list kept was screened out by a FULL list (its 32nd key, or its
+//      partner lane's, beats the row), so it ranks at or after the smallest 32nd key of any full
+//      list; the union's k-th key strictly below that floor proves the union's top-k is the
+//      corpus's.  With rows interleaved over the splits in 8-row groups a list holds ~k / lists of
+//      the answer (4 at k = 1024 over 256 lists), so the certificate fails only when one list's
+//      rows crowd the answer (or k approaches the corpus size);
+//   3. the queries it leaves (counted on the device, read back by the host: the one place this
+//      path waits for the GPU) are re-run by an exact scan: S stripes of the corpus per query,
+//      each a workgroup computing its rows' fp32 keys (one wave per row) into LDS and folding
+//      them into a running top-k with the same select, then the S lists merged.
+// Radix select (select_k): the values are u64 (order-preserving key bits | local row: unsigned
+// order = (key, row), faiss's tie rule); eight 8-bit digit passes of a 256-bin LDS histogram find
+// the k-th smallest T; the values < T, then copies of T, fill the result (empties = ~0 pad a
+// corpus with fewer than k rows); the last round sorts it bitonically.
 
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 #include <stdint.h>
 #include <float.h>
 #include <math.h>
@@ -95,84 +102,140 @@ __device__ void select_k(const uint64_t* v, int M, int k, uint64_t* sel, uint32_
         }
 }
 
-// Workgroup (query qq of the block, stripe s = blockIdx.y): the GEMM columns [s * nrc, (s + 1) *
-// nrc) of this round (ldg = the round's rows; global row r0 + s * nrc at column s * nrc) merged
-// into stripe s's running list run[(s * nq_all + q) * k ...].  With one stripe the last round
-// sorts and writes D / I; with several, largek_final_kernel merges the stripes.
-__global__ void __launch_bounds__(kLKThreads)
-largek_select_kernel(const float* __restrict__ G, int ldg, int nrc, const float* __restrict__ qnorm,
-                     const float* __restrict__ xn, int64_t r0, int k, int metric, int first,
-                     int last, int64_t q0, int64_t nq_all, uint64_t* __restrict__ run,
-                     float* __restrict__ D, int64_t* __restrict__ I, int64_t id_offset) {
-    __shared__ uint64_t v[kLKM];
-    __shared__ uint64_t sel[kLKSort];
-    __shared__ uint32_t hist[256];
-    __shared__ uint64_t s_prefix;
-    __shared__ int s_rem, s_nlt;
-    const int t = threadIdx.x;
-    const int64_t qq = blockIdx.x, q = q0 + qq;
-    const int sidx = blockIdx.y;
-    run += (int64_t)sidx * nq_all * k;
-    const int c0 = sidx * nrc;
-    const int ns = max(0, min(nrc, ldg - c0));          // this stripe's columns in the round
-    const int64_t rs = r0 + c0;
-    const int nr = first ? 0 : k;
-    for (int i = t; i < nr; i += kLKThreads) v[i] = run[q * k + i];
-    const float qn = qnorm[q];
-    const float* g = G + qq * (int64_t)ldg + c0;
-    for (int j = t; j < ns; j += kLKThreads) {
-        // L2: (|q|^2 + |x|^2) - 2 q.x, clamped at 0; IP: -q.x (G = -2 q.x, halving is exact)
-        const float key = metric == 1 ? fmaxf((qn + xn[rs + j]) + g[j], 0.f) : 0.5f * g[j];
-        v[nr + j] = ((uint64_t)key_bits_ordered(key) << 32) | (uint32_t)(rs + j);
-    }
-    const int M = nr + ns;
-    select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, last != 0);
-    if (!last) {
-        for (int i = t; i < k; i += kLKThreads) run[q * k + i] = sel[i];
-        return;
-    }
-    for (int i = t; i < k; i += kLKThreads) {
+// Output of a finished top-k list: row q of D / I from sel[0 .. k) (local rows + id_offset).
+__device__ void write_topk(const uint64_t* sel, int k, int metric, int64_t id_offset, float* D,
+                           int64_t* I) {
+    for (int i = threadIdx.x; i < k; i += kLKThreads) {
         const uint64_t x = sel[i];
         if (x == ~0ull) {
-            D[q * k + i] = metric == 1 ? FLT_MAX : -FLT_MAX;
-            I[q * k + i] = -1;
+            D[i] = metric == 1 ? FLT_MAX : -FLT_MAX;
+            I[i] = -1;
         } else {
             const float key = key_from_ordered((uint32_t)(x >> 32));
-            D[q * k + i] = metric == 1 ? key : -key;
-            I[q * k + i] = (int64_t)(uint32_t)x + id_offset;
+            D[i] = metric == 1 ? key : -key;
+            I[i] = (int64_t)(uint32_t)x + id_offset;
         }
     }
 }
 
-// The stripes' running lists of one query (S x k local rows) -> the final sorted top-k.
+// Step 2 (module doc): a workgroup per query of the block.  cd / ci: the tile kernel's lists
+// (nlists of km ascending keys per query, stride ncand; labels with id_offset, -1 = empty).
+// Certified queries are written to D / I; the others go to fail_list (with their union's k-th
+// value, the fallback's bound) — fail_cnt counts them.
 __global__ void __launch_bounds__(kLKThreads)
-largek_final_kernel(const uint64_t* __restrict__ run, int S, int64_t nq_all, int k, int64_t q0,
-                    int metric, float* __restrict__ D, int64_t* __restrict__ I, int64_t id_offset) {
+largek_union_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int nlists, int km,
+                    int ncand, int k, int64_t ntotal, int metric, int64_t id_offset,
+                    float* __restrict__ D, int64_t* __restrict__ I, int* __restrict__ fail_list,
+                    int* __restrict__ fail_cnt) {
     __shared__ uint64_t v[kLKM];
     __shared__ uint64_t sel[kLKSort];
     __shared__ uint32_t hist[256];
     __shared__ uint64_t s_prefix;
     __shared__ int s_rem, s_nlt;
+    __shared__ uint32_t s_floor;
     const int t = threadIdx.x;
-    const int64_t q = q0 + blockIdx.x;
-    const int M = S * k;
-    for (int e = t; e < M; e += kLKThreads) {
-        const int sidx = e / k, i = e - sidx * k;
-        v[e] = run[((int64_t)sidx * nq_all + q) * k + i];
+    const int64_t q = blockIdx.x;
+    const float* qd = cd + q * (int64_t)ncand;
+    const int64_t* qi = ci + q * (int64_t)ncand;
+    if (t == 0) s_floor = ~0u;
+    __syncthreads();
+    const int M = nlists * km, C = kLKM - k;
+    int nr = 0;
+    for (int c0 = 0; c0 < M; c0 += C) {
+        const int cn = min(C, M - c0);
+        for (int i = t; i < nr; i += kLKThreads) v[i] = sel[i];
+        for (int e = t; e < cn; e += kLKThreads) {
+            const int idx = c0 + e;
+            const int64_t lab = qi[idx];
+            const uint32_t kb = key_bits_ordered(qd[idx]);
+            v[nr + e] = lab < 0 ? ~0ull : ((uint64_t)kb << 32) | (uint32_t)(lab - id_offset);
+            // the last entry of a FULL list bounds every row that list (or its partner) dropped
+            if (idx % km == km - 1 && lab >= 0) atomicMin(&s_floor, kb);
+        }
+        __syncthreads();
+        select_k(v, nr + cn, k, sel, hist, &s_prefix, &s_rem, &s_nlt, c0 + C >= M);
+        nr = k;
     }
+    const int kk = (int)min<int64_t>(k, ntotal);
+    const uint64_t T = sel[kk - 1];
+    const bool ok = s_floor == ~0u || (T != ~0ull && (uint32_t)(T >> 32) < s_floor);
+    if (ok) {
+        write_topk(sel, k, metric, id_offset, D + q * k, I + q * k);
+    } else if (t == 0) {
+        fail_list[atomicAdd(fail_cnt, 1)] = (int)q;
+    }
+}
+
+// Step 3, a workgroup per (stripe s = blockIdx.x, failing query f = blockIdx.y): the exact fp32
+// keys of rows [s R, (s + 1) R) — one wave per row, lanes over the row's float4s, a shuffle
+// reduction — folded chunk by chunk into a running top-k (select_k), written to
+// run[(f S + s) k ...].  qpad / qnorm: the query block's padded rows and norms.
+__global__ void __launch_bounds__(kLKThreads)
+largek_scan_kernel(const float* __restrict__ xb, const float* __restrict__ xn, int64_t ntotal, int dp,
+                   const float* __restrict__ qpad, const float* __restrict__ qnorm,
+                   const int* __restrict__ fail_list, int f0, int64_t R, int k, int metric,
+                   uint64_t* __restrict__ run) {
+    __shared__ uint64_t v[kLKM];
+    __shared__ uint64_t sel[kLKSort];
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t s_prefix;
+    __shared__ int s_rem, s_nlt;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int S = gridDim.x, s = blockIdx.x, f = blockIdx.y;
+    const int q = fail_list[f0 + f];
+    const float4* q4 = reinterpret_cast<const float4*>(qpad + (int64_t)q * dp);
+    const float qn = qnorm[q];
+    const int64_t r0 = (int64_t)s * R, r1 = min(ntotal, r0 + R);
+    const int C = kLKM - k;
+    const int nv4 = dp / 4;
+    int nr = 0;
+    for (int64_t c0 = r0; c0 < r1 || (c0 == r0 && nr == 0); c0 += C) {
+        const int cn = (int)max<int64_t>(0, min<int64_t>(C, r1 - c0));
+        for (int i = t; i < nr; i += kLKThreads) v[i] = sel[i];
+        for (int j = wave; j < cn; j += kLKThreads / 64) {
+            const int64_t row = c0 + j;
+            const float4* x4 = reinterpret_cast<const float4*>(xb + row * dp);
+            float acc = 0.f;
+            for (int c = lane; c < nv4; c += 64) {
+                const float4 a = x4[c], b = q4[c];
+                acc = fmaf(a.x, b.x, acc);
+                acc = fmaf(a.y, b.y, acc);
+                acc = fmaf(a.z, b.z, acc);
+                acc = fmaf(a.w, b.w, acc);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+            if (lane == 0) {
+                // L2: (|q|^2 + |x|^2) - 2 q.x, clamped at 0; IP: -q.x
+                const float key = metric == 1 ? fmaxf((qn + xn[row]) - 2.f * acc, 0.f) : -acc;
+                v[nr + j] = ((uint64_t)key_bits_ordered(key) << 32) | (uint32_t)row;
+            }
+        }
+        __syncthreads();
+        select_k(v, nr + cn, k, sel, hist, &s_prefix, &s_rem, &s_nlt, false);
+        nr = k;
+        if (cn == 0) break;
+    }
+    uint64_t* out = run + ((int64_t)f * S + s) * k;
+    for (int i = t; i < k; i += kLKThreads) out[i] = sel[i];
+}
+
+// The S stripe lists of failing query f (S * k <= kLKM) -> its final sorted top-k in D / I.
+__global__ void __launch_bounds__(kLKThreads)
+largek_final_kernel(const uint64_t* __restrict__ run, int S, int k, const int* __restrict__ fail_list,
+                    int f0, int metric, int64_t id_offset, float* __restrict__ D, int64_t* __restrict__ I) {
+    __shared__ uint64_t v[kLKM];
+    __shared__ uint64_t sel[kLKSort];
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t s_prefix;
+    __shared__ int s_rem, s_nlt;
+    const int t = threadIdx.x, f = blockIdx.x;
+    const int q = fail_list[f0 + f];
+    const int M = S * k;
+    for (int e = t; e < M; e += kLKThreads) v[e] = run[(int64_t)f * M + e];
     __syncthreads();
     select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, true);
-    for (int i = t; i < k; i += kLKThreads) {
-        const uint64_t x = sel[i];
-        if (x == ~0ull) {
-            D[q * k + i] = metric == 1 ? FLT_MAX : -FLT_MAX;
-            I[q * k + i] = -1;
-        } else {
-            const float key = key_from_ordered((uint32_t)(x >> 32));
-            D[q * k + i] = metric == 1 ? key : -key;
-            I[q * k + i] = (int64_t)(uint32_t)x + id_offset;
-        }
-    }
+    write_topk(sel, k, metric, id_offset, D + (int64_t)q * k, I + (int64_t)q * k);
 }
 
 // Merge of nlists sorted per-shard results of kin entries per query (distance-ascending for L2,
@@ -225,12 +288,10 @@ hipError_t launch_merge_large(const float* cD, const int64_t* cI, int nlists, in
 }
 
 void largek_free(knn_index* ix) {
-    if (ix->blas) (void)rocblas_destroy_handle((rocblas_handle)ix->blas);
-    ix->blas = nullptr;
-    for (void* p : {(void*)ix->lk_g, (void*)ix->lk_run})
+    for (void* p : {(void*)ix->lk_run, (void*)ix->lk_fail})
         if (p) (void)hipFree(p);
-    ix->lk_g = nullptr;
     ix->lk_run = nullptr;
+    ix->lk_fail = nullptr;
 }
 
 int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
@@ -243,50 +304,51 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         return KNN_OK;
     }
     int rc;
-    // Small batches: S stripes of running lists per query, so one GEMM round covers S corpus
-    // blocks (S x fewer GEMM + select launches, S workgroups per query) and a final kernel merges
-    // the S lists (S * k <= kLKM).  Large batches fill the chip with one stripe.
-    const int S = nq <= 64 ? (int)std::max<int64_t>(1, std::min<int64_t>(32, kLKM / k)) : 1;
-    const int64_t nqc = std::min<int64_t>(nq, 2048);       // queries per GEMM block
-    const int nrc_max = kLKM - k;
-    const int64_t round_rows = (int64_t)S * nrc_max;
-    // workspace sized for ONE query block (queries, norms, GEMM block, running lists), reused
-    // by every block: independent of the batch size
-    if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)nqc * ix->dp)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)nqc)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->lk_g, &ix->lk_g_cap, (size_t)nqc * round_rows)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)S * nqc * k)) != KNN_OK) return rc;
-    if (!ix->blas) {
-        rocblas_handle h;
-        if (rocblas_create_handle(&h) != rocblas_status_success)
-            KNN_FAIL(KNN_EHIP, "rocblas_create_handle failed");
-        ix->blas = h;
-    }
-    const rocblas_handle h = (rocblas_handle)ix->blas;
-    if (rocblas_set_stream(h, st) != rocblas_status_success) KNN_FAIL(KNN_EHIP, "rocblas_set_stream failed");
-    const float alpha = -2.f, beta = 0.f;
-    for (int64_t q0 = 0; q0 < nq; q0 += nqc) {
-        const int qc = (int)std::min<int64_t>(nqc, nq - q0);
-        KNN_HIP(launch_rows_ingest(q + q0 * ix->d, qc, ix->d, ix->dp, qc,
+    ix->lk_last_fallbacks = 0;
+    // fallback geometry: S stripes per failing query (S k <= kLKM for the final merge), at most
+    // kLKFail failing queries per scan launch
+    const int S = (int)std::max<int64_t>(1, std::min<int64_t>({64, kLKM / k, (ix->ntotal + 1023) / 1024}));
+    const int64_t R = (ix->ntotal + S - 1) / S;
+    constexpr int kLKFail = 64;
+    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)kLKFail * S * k)) != KNN_OK) return rc;
+    for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
+        const int64_t qc = std::min<int64_t>(kQueryChunk, nq - q0);
+        const Plan p = make_plan(ix->ntotal, qc, KNN_MAX_K, ix->cus);     // KM = 32 lists
+        if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)p.nq_pad)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)qc * p.ncand)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)qc * p.ncand)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->lk_fail, &ix->lk_fail_cap, (size_t)qc + 1)) != KNN_OK) return rc;
+        KNN_HIP(launch_rows_ingest(q + q0 * ix->d, qc, ix->d, ix->dp, p.nq_pad,
                                    ix->metric == KNN_METRIC_COSINE ? 1 : 0, ix->qpad, ix->qnorm, st));
-        float* Db = D + q0 * k;          // the block's outputs; the kernels index it from 0
+        TileArgs a{};
+        a.wr = p.wr; a.wq = p.wq; a.km = p.km;
+        a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
+        a.qp = ix->qpad; a.qnorm = ix->qnorm; a.nq = (int)qc; a.metric = kmetric;
+        a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
+        a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.mode = kModeF32;
+        KNN_HIP(launch_tile_topk(a, st));
+        float* Db = D + q0 * k;
         int64_t* Ib = I + q0 * k;
-        for (int64_t r0 = 0; r0 < ix->ntotal; r0 += round_rows) {
-            const int m = (int)std::min<int64_t>(round_rows, ix->ntotal - r0);
-            // column-major: G (m x qc, ld m) = X_rows^T (m x dp) * Q_block (dp x qc)
-            if (rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, m, qc, ix->dp,
-                              &alpha, ix->xb + r0 * ix->dp, ix->dp, ix->qpad, ix->dp,
-                              &beta, ix->lk_g, m) != rocblas_status_success)
-                KNN_FAIL(KNN_EHIP, "rocblas_sgemm failed");
-            const int last = (S == 1 && r0 + m >= ix->ntotal) ? 1 : 0;
-            hipLaunchKernelGGL(largek_select_kernel, dim3((unsigned)qc, (unsigned)S), dim3(kLKThreads), 0, st,
-                               ix->lk_g, m, nrc_max, ix->qnorm, ix->xn, r0, k, kmetric, r0 == 0 ? 1 : 0,
-                               last, (int64_t)0, nqc, ix->lk_run, Db, Ib, ix->id_offset);
+        int* cnt = ix->lk_fail + qc;
+        KNN_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
+        hipLaunchKernelGGL(largek_union_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st, ix->cand_d,
+                           ix->cand_i, p.ncand / p.km, p.km, p.ncand, k, ix->ntotal, kmetric,
+                           ix->id_offset, Db, Ib, ix->lk_fail, cnt);
+        KNN_HIP(hipGetLastError());
+        // the certificate's leftovers: the host reads their count (this path's only wait)
+        int nfail = 0;
+        KNN_HIP(hipMemcpyAsync(&nfail, cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+        KNN_HIP(hipStreamSynchronize(st));
+        ix->lk_last_fallbacks += nfail;
+        for (int f0 = 0; f0 < nfail; f0 += kLKFail) {
+            const int nf = std::min(kLKFail, nfail - f0);
+            hipLaunchKernelGGL(largek_scan_kernel, dim3((unsigned)S, (unsigned)nf), dim3(kLKThreads), 0, st,
+                               ix->xb, ix->xn, ix->ntotal, ix->dp, ix->qpad, ix->qnorm, ix->lk_fail, f0, R,
+                               k, kmetric, ix->lk_run);
             KNN_HIP(hipGetLastError());
-        }
-        if (S > 1) {
-            hipLaunchKernelGGL(largek_final_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st,
-                               ix->lk_run, S, nqc, k, (int64_t)0, kmetric, Db, Ib, ix->id_offset);
+            hipLaunchKernelGGL(largek_final_kernel, dim3((unsigned)nf), dim3(kLKThreads), 0, st, ix->lk_run, S,
+                               k, ix->lk_fail, f0, kmetric, ix->id_offset, Db, Ib);
             KNN_HIP(hipGetLastError());
         }
     }

@@ -119,10 +119,13 @@ enum knn_search_mode {
 
 /* Largest k the fused top-k kernels serve (they keep per-lane lists of this length). */
 #define KNN_MAX_K 32
-/* Largest k one search can return: KNN_MAX_K < k <= KNN_MAX_K_LARGE runs faiss IndexFlat's own
- * algorithm (fp32 GEMM blocks + an exact per-query radix select, csrc/knn_largek.hip); a
- * multi-device index (knn_create_multi) runs it on every shard and merges the shards' k-lists with
- * the same select (at most 8192 gathered entries per query). */
+/* Largest k one search can return: KNN_MAX_K < k <= KNN_MAX_K_LARGE runs the exact fp32 fused
+ * kernel with 32-entry lists, the k best of their union by an exact per-query radix select,
+ * certified against the lists' floor; the queries the certificate cannot settle are re-run by an
+ * exact corpus scan (csrc/knn_largek.hip: no key block ever reaches HBM).  This is the one search
+ * path that reads a count back to the host (device entry points included): once per 8192-query
+ * chunk.  A multi-device index (knn_create_multi) runs it on every shard and merges the shards'
+ * k-lists with the same select (at most 8192 gathered entries per query). */
 #define KNN_MAX_K_LARGE 1024
 
 /* Create an empty index of dimension d on HIP device `device` (-1 = current device). */
@@ -212,6 +215,11 @@ int knn_search_stats2(knn_index_t* index, int64_t* split_queries, int64_t* fallb
 /* Arithmetic the last search's first query chunk ran: 0 = exact fp32 kernel, 1 = split path,
  * 2 = bf16 path, 3 = int8 path (the candidate paths' fallbacks are counted by knn_search_stats). */
 int knn_last_path(const knn_index_t* index);
+
+/* Queries of the last k > KNN_MAX_K search that its certificate could not settle from the fused
+ * kernel's 32-entry lists and that were re-run by the exact corpus scan (csrc/knn_largek.hip);
+ * summed over the shards of a multi-device index. */
+int knn_large_k_fallbacks(const knn_index_t* index, int64_t* queries);
 
 /* Launch geometry chosen for a search of nq queries (for reports): workgroup tile rows/queries,
  * row splits and workgroup count. */
