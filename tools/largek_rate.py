@@ -1,4 +1,5 @@
-"""Large-k search rate (k > KNN_MAX_K: csrc/knn_largek.hip, fp32 GEMM + radix select) on the
+"""Large-k search rate (k > KNN_MAX_K: csrc/knn_largek.hip, exact fused kernel lists + certified
+radix-select union + exact-scan fallback) on the
 bench corpus (config 3, 1M x 1968), nq = 1 and 1024.  Measurement tool; one JSON line per case."""
 import json
 import os
@@ -28,5 +29,9 @@ for nq, k, reps in ((1, 100, 10), (1024, 100, 3), (1024, 1024, 2)):
         shard.search(q, k)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / reps * 1e3
-    print(json.dumps({"rows": cfg["rows"], "d": D, "nq": nq, "k": k, "ms": ms, "qps": nq / ms * 1e3,
-                      "gemm_tflops": 2.0 * cfg["rows"] * D * nq / (ms * 1e-3) / 1e12}), flush=True)
+    from image_recommender_amd import _lib
+    import ctypes as C
+    nf = C.c_int64()
+    _lib.load().knn_large_k_fallbacks(shard.index.handle, C.byref(nf))
+    print(json.dumps({"rows": cfg["rows"], "d": D, "nq": nq, "k": k, "ms": ms, "qps": nq / ms * 1e3, "fallbacks": nf.value,
+                      "fp32_tflops": 2.0 * cfg["rows"] * D * nq / (ms * 1e-3) / 1e12}), flush=True)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""One-query search time on 1M-row corpora of small widths (colour-only d = 48, SIFT-only 128):
+"""One-query search time on 1M-row corpora of small widths (colour-only d = 48, SIFT-only 128;
+WIDTHS=48,128,512 adds d = 512, the int8 gate's 8-block boundary):
 device-resident queries through search_device, median of 200 searches; the path AUTO takes
 (knn_last_path: 0 exact, 2 bf16, 3 int8).  Measurement tool, one JSON line per width."""
 import json
@@ -14,7 +15,7 @@ from image_recommender_amd import _lib, faiss_compat as faiss  # noqa: E402
 
 torch.cuda.set_device(0)
 n = int(os.environ.get("ROWS", 1_000_000))
-for d in (48, 128):
+for d in [int(w) for w in os.environ.get("WIDTHS", "48,128").split(",")]:
     g = torch.Generator(device="cuda").manual_seed(d)
     xb = torch.randn((n, d), device="cuda", generator=g)
     idx = faiss.IndexFlatL2(d)
@@ -24,7 +25,7 @@ for d in (48, 128):
     q = torch.randn((1, d), device="cuda", generator=g)
     D = torch.empty((1, 10), dtype=torch.float32, device="cuda")
     I = torch.empty((1, 10), dtype=torch.int64, device="cuda")
-    for modes in (("auto", "exact") if d < 64 else ("auto", "exact", "bf16")):
+    for modes in (("auto", "exact") if d < 64 else ("auto", "exact", "bf16", "i8")):
         idx.search_mode = modes
         ts = []
         for i in range(250):
