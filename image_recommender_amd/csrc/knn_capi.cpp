@@ -280,6 +280,7 @@ int create_single(int d, int metric, int device, knn_index** out) {
         ix->merge_fuse1 = *e != '0' && *e != '1';
     }
     if (const char* e = test_knob("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
+    if (const char* e = test_knob("IMGREC_I8_FUSED_PREP")) ix->i8_fused_prep = *e != '0';
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ix->fence, hipEventDisableTiming) != hipSuccess) {
         if (ix->stream) (void)hipStreamDestroy(ix->stream);

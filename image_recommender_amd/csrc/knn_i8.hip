@@ -44,6 +44,9 @@ constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA pi
 #define IMGREC_I8_NT 1
 #endif
 constexpr bool kNtCodes = IMGREC_I8_NT != 0;   // non-temporal code loads in the scan
+#ifndef IMGREC_I8_PRELOAD
+#define IMGREC_I8_PRELOAD 1
+#endif
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -108,6 +111,49 @@ i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t
     xsq = wave_sum(xsq);
     // |fl(c s) - c s| <= 2^-24 |c s| per element: 2^-22 |x| covers the evaluation of every term
     if (lane == 0) resid[row] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
+}
+
+// Two-level int8 codes of one 64-element query block, q~ = s_hi c_hi + s_lo c_lo (c_hi =
+// rint(v / s_hi), s_hi = max|v| / 127; c_lo the same of v - s_hi c_hi): emit(lev, e4, word) gets
+// the codes of elements 4 e4 .. 4 e4 + 3 of level lev (0 = hi) as they are made, sc = (s_hi,
+// s_lo); v ends as the residual v - q~; xsq += |v|^2 and rsq += |v - q~|^2.  The one quantiser of
+// i8_query_prep_kernel and the scan's fused prep (bit-identical by construction; the scan writes
+// each word straight to LDS, so no code words are held in registers).
+template <class Emit>
+__device__ __forceinline__ void quantize_query_block(float (&v)[kBlk], Emit&& emit, float (&sc)[2],
+                                                     float& xsq, float& rsq) {
+    float mx = 0.f;
+#pragma unroll
+    for (int t = 0; t < kBlk; ++t) {
+        mx = fmaxf(mx, fabsf(v[t]));
+        xsq = fmaf(v[t], v[t], xsq);
+    }
+#pragma unroll
+    for (int lev = 0; lev < 2; ++lev) {
+        const float sl = mx / 127.f, inv = mx > 0.f ? 127.f / mx : 0.f;
+        float mx2 = 0.f;
+#pragma unroll
+        for (int e4 = 0; e4 < kBlk / 4; ++e4) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int c = max(-127, min(127, (int)rintf(v[4 * e4 + t] * inv)));
+                v[4 * e4 + t] -= (float)c * sl;              // the residual, next level's input
+                mx2 = fmaxf(mx2, fabsf(v[4 * e4 + t]));
+                word |= ((uint32_t)c & 0xffu) << (8 * t);
+            }
+            emit(lev, e4, word);
+        }
+        sc[lev] = sl;
+        mx = mx2;
+    }
+#pragma unroll
+    for (int t = 0; t < kBlk; ++t) rsq = fmaf(v[t], v[t], rsq);
+}
+
+// |q - q~| bound from the block sums (inflated for its own fp32 evaluation as the rows' is)
+__device__ __forceinline__ float query_resid(float rsq, float xsq) {
+    return sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
 }
 
 // The int8 path's whole query side in one pass (one wave per query row): raw row (d floats) ->
@@ -182,37 +228,12 @@ i8_query_prep_kernel(const float* __restrict__ src, int64_t n, int d, int dp, in
     __syncthreads();
     float rsq = 0.f, xsq = 0.f;
     if (lane < nblk) {
-        float v[kBlk];
-        float mx = 0.f;
-#pragma unroll
-        for (int t = 0; t < kBlk; ++t) {
-            v[t] = srow[lane * kPitch + t];
-            mx = fmaxf(mx, fabsf(v[t]));
-            xsq = fmaf(v[t], v[t], xsq);
-        }
         uint32_t w[2][kBlk / 4];
         float sc[2];
+        float v[kBlk];
 #pragma unroll
-        for (int lev = 0; lev < 2; ++lev) {
-            const float sl = mx / 127.f, inv = mx > 0.f ? 127.f / mx : 0.f;
-            float mx2 = 0.f;
-#pragma unroll
-            for (int e4 = 0; e4 < kBlk / 4; ++e4) {
-                uint32_t word = 0;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int c = max(-127, min(127, (int)rintf(v[4 * e4 + t] * inv)));
-                    v[4 * e4 + t] -= (float)c * sl;              // the residual, next level's input
-                    mx2 = fmaxf(mx2, fabsf(v[4 * e4 + t]));
-                    word |= ((uint32_t)c & 0xffu) << (8 * t);
-                }
-                w[lev][e4] = word;
-            }
-            sc[lev] = sl;
-            mx = mx2;
-        }
-#pragma unroll
-        for (int t = 0; t < kBlk; ++t) rsq = fmaf(v[t], v[t], rsq);
+        for (int t = 0; t < kBlk; ++t) v[t] = srow[lane * kPitch + t];
+        quantize_query_block(v, [&](int lev, int e4, uint32_t word) { w[lev][e4] = word; }, sc, xsq, rsq);
         uint4* out = reinterpret_cast<uint4*>(codes + (row * nblk + lane) * 2 * kBlk);
 #pragma unroll
         for (int c = 0; c < 8; ++c)
@@ -223,7 +244,7 @@ i8_query_prep_kernel(const float* __restrict__ src, int64_t n, int d, int dp, in
     }
     rsq = wave_sum(rsq);
     xsq = wave_sum(xsq);
-    if (lane == 0) resid[row] = sqrtf(rsq) * (1.f + 1.f / 65536.f) + sqrtf(xsq) * (1.f / 4194304.f);
+    if (lane == 0) resid[row] = query_resid(rsq, xsq);
 }
 
 // Ascending list, labels arriving in increasing order: slot p's key is the median of (kd[p-1], d,
@@ -250,7 +271,9 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
                    const int8_t* __restrict__ qcodes, const float* __restrict__ qscales,
                    const float* __restrict__ qnorm, int nq,
                    int nsplit, int64_t id_offset, int l2, float* __restrict__ cand_d,
-                   int64_t* __restrict__ cand_i, int ncand) {
+                   int64_t* __restrict__ cand_i, int ncand, const float* __restrict__ qsrc, int d,
+                   int dp, int normalize, float* __restrict__ qpad, float* __restrict__ qnorm_out,
+                   float* __restrict__ qresid) {
     // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
     // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
     // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
@@ -271,23 +294,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = lane & 15, g = lane >> 4;
     const int64_t rowb = i8_row_bytes(nblk);
-    for (int i = tid; i < NQ * 16 * NBI * 8; i += kWaves * 64) {          // 16-B chunks
-        const int qi = i / (16 * NBI * 8), r = i - qi * (16 * NBI * 8), b = r >> 3, c = r & 7;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (qi < nq && b < nblk) v = reinterpret_cast<const uint4*>(qcodes + ((int64_t)qi * nblk + b) * 2 * kBlk)[c];
-        *reinterpret_cast<uint4*>(&sqc[qi][b][16 * c]) = v;
-    }
-    for (int i = tid; i < NQ * 16 * NBI; i += kWaves * 64) {
-        const int qi = i / (16 * NBI), b = i - qi * (16 * NBI);
-        const bool in = qi < nq && b < nblk;
-        sqs[qi][b][0] = in ? qscales[((int64_t)qi * nblk + b) * 2] : 0.f;
-        sqs[qi][b][1] = in ? qscales[((int64_t)qi * nblk + b) * 2 + 1] : 0.f;
-    }
     float qn[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) qn[q] = (l2 && q < nq) ? qnorm[q] : 0.f;
-    __syncthreads();
-
     float kd[KM];
     int ki[KM];
 #pragma unroll
@@ -417,9 +424,131 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
             if (__any(kv != INFINITY)) insert_mono<KM>(kd, ki, kv, G.row[h]);
         }
     };
+    // the first group's code loads go out before the query side is ready (IMGREC_I8_PRELOAD):
+    // their HBM round trip overlaps the fused prep's quantising or the codes' copy into LDS
     Grp A, B;
     int li = wave;
-    if (li < cnt) load(li, A);
+    // (only where the group's codes are <= 32 registers: holding 64 across the prep spills)
+    constexpr bool kPre = IMGREC_I8_PRELOAD && H * NBI <= 2 && NQ <= 4;
+    if (kPre && li < cnt) load(li, A);
+    __shared__ float s_qn[NQ];
+    if (qsrc) {
+        // Fused query prep (I8Args::qsrc): wave w derives queries w, w + 4 from the raw rows with
+        // i8_query_prep_kernel's arithmetic — the same lane chunks and reductions for the row, its
+        // norm and scale, the same quantiser per block — straight into this workgroup's LDS;
+        // workgroup 0 also writes the padded fp32 rows, |q|^2 and |q - q~| for the rerank and
+        // the tail.  (One launch and its dependent gap fewer per search; every workgroup repeats
+        // ~1 us of quantising that overlaps the other waves' first code loads.)
+        for (int i = tid; i < NQ * 16 * NBI * 8; i += kWaves * 64) {      // what no query fills
+            const int qi = i / (16 * NBI * 8), r = i - qi * (16 * NBI * 8), b = r >> 3, c = r & 7;
+            if (qi >= nq || b >= nblk) *reinterpret_cast<uint4*>(&sqc[qi][b][16 * c]) = make_uint4(0u, 0u, 0u, 0u);
+        }
+        for (int i = tid; i < NQ * 16 * NBI; i += kWaves * 64) {
+            const int qi = i / (16 * NBI), b = i - qi * (16 * NBI);
+            if (qi >= nq || b >= nblk) { sqs[qi][b][0] = 0.f; sqs[qi][b][1] = 0.f; }
+        }
+#pragma unroll 1
+        for (int qi = wave; qi < NQ && qi < nq; qi += kWaves) {
+            const float* s = qsrc + (int64_t)qi * d;
+            // the row in i8_query_prep_kernel's chunks (lane c: elements 8c .. 8c + 7; chunks past
+            // dp add exact zeros there, so they are skipped here)
+            auto chunk = [&](int c, float (&e)[8]) __attribute__((always_inline)) {
+                const int j0 = 8 * c;
+                if ((d & 3) == 0 && j0 + 8 <= d) {
+                    const float4 v0 = *reinterpret_cast<const float4*>(s + j0);
+                    const float4 v1 = *reinterpret_cast<const float4*>(s + j0 + 4);
+                    e[0] = v0.x; e[1] = v0.y; e[2] = v0.z; e[3] = v0.w;
+                    e[4] = v1.x; e[5] = v1.y; e[6] = v1.z; e[7] = v1.w;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) e[t] = j0 + t < d ? s[j0 + t] : 0.f;
+                }
+            };
+            float scale = 1.f;
+            if (normalize) {
+                float acc = 0.f;
+                for (int c = lane; 8 * c < dp; c += 64) {
+                    float e[8];
+                    chunk(c, e);
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) acc = fmaf(e[t], e[t], acc);
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+                if (acc > 0.f) scale = (float)(1.0 / (double)sqrtf(acc));
+            }
+            float nacc = 0.f;
+            for (int c = lane; 8 * c < dp; c += 64) {
+                float e[8];
+                chunk(c, e);
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    e[t] = normalize ? e[t] * scale : e[t];
+                    nacc = fmaf(e[t], e[t], nacc);
+                }
+                if (split == 0) {
+                    float* o = qpad + (int64_t)qi * dp + 8 * c;
+                    *reinterpret_cast<float4*>(o) = make_float4(e[0], e[1], e[2], e[3]);
+                    *reinterpret_cast<float4*>(o + 4) = make_float4(e[4], e[5], e[6], e[7]);
+                }
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) nacc += __shfl_xor(nacc, off, 64);
+            float rsq = 0.f, xsq = 0.f;
+            if (lane < nblk) {
+                // lane b's block from the raw row (L1 / L2 after the chunk pass), scaled as the
+                // chunk pass scaled it (the same product); elements past d are zero
+                const int i0 = lane * kBlk;
+                float v[kBlk];
+                if ((d & 3) == 0 && i0 + kBlk <= d) {
+#pragma unroll
+                    for (int t4 = 0; t4 < kBlk / 4; ++t4) {
+                        const float4 x4 = *reinterpret_cast<const float4*>(s + i0 + 4 * t4);
+                        v[4 * t4] = x4.x; v[4 * t4 + 1] = x4.y; v[4 * t4 + 2] = x4.z; v[4 * t4 + 3] = x4.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int t = 0; t < kBlk; ++t) v[t] = i0 + t < d ? s[i0 + t] : 0.f;
+                }
+                if (normalize) {
+#pragma unroll
+                    for (int t = 0; t < kBlk; ++t) v[t] = v[t] * scale;
+                }
+                float sc[2];
+                uint32_t* qw = reinterpret_cast<uint32_t*>(&sqc[qi][lane][0]);
+                quantize_query_block(v, [&](int lev, int e4, uint32_t word) { qw[lev * (kBlk / 4) + e4] = word; },
+                                     sc, xsq, rsq);
+                sqs[qi][lane][0] = sc[0];
+                sqs[qi][lane][1] = sc[1];
+            }
+            if (lane == 0) s_qn[qi] = nacc;
+            if (split == 0) {
+                rsq = wave_sum(rsq);
+                xsq = wave_sum(xsq);
+                if (lane == 0) { qnorm_out[qi] = nacc; qresid[qi] = query_resid(rsq, xsq); }
+            }
+        }
+    } else {
+        for (int i = tid; i < NQ * 16 * NBI * 8; i += kWaves * 64) {          // 16-B chunks
+            const int qi = i / (16 * NBI * 8), r = i - qi * (16 * NBI * 8), b = r >> 3, c = r & 7;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (qi < nq && b < nblk) v = reinterpret_cast<const uint4*>(qcodes + ((int64_t)qi * nblk + b) * 2 * kBlk)[c];
+            *reinterpret_cast<uint4*>(&sqc[qi][b][16 * c]) = v;
+        }
+        for (int i = tid; i < NQ * 16 * NBI; i += kWaves * 64) {
+            const int qi = i / (16 * NBI), b = i - qi * (16 * NBI);
+            const bool in = qi < nq && b < nblk;
+            sqs[qi][b][0] = in ? qscales[((int64_t)qi * nblk + b) * 2] : 0.f;
+            sqs[qi][b][1] = in ? qscales[((int64_t)qi * nblk + b) * 2 + 1] : 0.f;
+        }
+        if (tid < NQ) s_qn[tid] = tid < nq ? qnorm[tid] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)      // (uniform: scalar registers, as the kernel-argument loads were)
+        qn[q] = (l2 && q < nq) ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_qn[q]))) : 0.f;
+
+    if (!kPre && li < cnt) load(li, A);
     while (li < cnt) {
         if (li + kWaves < cnt) load(li + kWaves, B);
         process(A);
@@ -497,13 +626,18 @@ hipError_t launch_i8_query_prep(const float* src, int64_t n, int d, int dp, int6
 
 hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
     if (a.nblk <= 0 || a.nblk > 64 || a.nq < 1 || a.nsplit < 1) return hipErrorInvalidValue;
+    if (a.qsrc && (a.dp % 16 != 0 || a.dp < a.d || a.d < 1 || a.dp > a.nblk * kBlk || !a.qpad ||
+                   !a.qnorm_out || !a.qresid))
+        return hipErrorInvalidValue;
+    if (!a.qsrc && (!a.qcodes || !a.qscales || !a.qnorm)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);
     const int nbi = (a.nblk + 15) / 16;
 #define IMGREC_I8(NQV, KMV, NBIV)                                                                 \
     hipLaunchKernelGGL((knn_i8_scan_kernel<NQV, KMV, NBIV>), grid, block, 0, st, a.codes, a.scales, \
                        a.xnorm, a.nrows, a.nblk, a.qcodes, a.qscales, a.qnorm, a.nq, a.nsplit,      \
                        a.id_offset,                                                                 \
-                       a.l2, a.cand_d, a.cand_i, a.ncand)
+                       a.l2, a.cand_d, a.cand_i, a.ncand, a.qsrc, a.d, a.dp, a.normalize, a.qpad,  \
+                       a.qnorm_out, a.qresid)
 #define IMGREC_I8_NBI(NQV, KMV)                                   \
     do {                                                          \
         switch (nbi) {                                            \

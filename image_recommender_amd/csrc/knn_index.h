@@ -102,6 +102,7 @@ struct knn_index {
     int i8_wgpcu = imgrec::kI8WGPCUDefault;
     bool merge_fuse = true;
     bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
+    bool i8_fused_prep = true;  // int8 query prep inside the scan (IMGREC_I8_FUSED_PREP=0: own launch)
     bool merge_fuse1 = true;    // IMGREC_MERGE_FUSE=1: only level 2 in the rerank (0: neither)
     int64_t ntotal = 0, cap = 0, id_offset = 0;
     bool trained = true;

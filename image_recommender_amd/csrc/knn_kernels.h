@@ -198,6 +198,15 @@ struct I8Args {
     float* cand_d;              // nq x ncand keys, one sorted list of km per split
     int64_t* cand_i;
     int ncand;
+    // Fused query prep (qsrc non-NULL; qcodes / qscales / qnorm unused): the raw query rows (nq x
+    // d); the scan quantises them itself and workgroup 0 writes what launch_i8_query_prep would
+    // for the rerank: the padded fp32 rows (nq x dp, L2-normalised when `normalize`), |q|^2 and
+    // |q - q~|.  (The codes themselves are consumed by the scan only.)
+    const float* qsrc;
+    int d, dp, normalize;
+    float* qpad;
+    float* qnorm_out;
+    float* qresid;
 };
 // Bytes per row of the int8 copy: 64 per block, no padding (round 4; rows were whole 1-KiB
 // groups of 16 blocks, 25 % zeros at d = 768).  Blocks sit in groups of 16 (the scan's 16 lanes of

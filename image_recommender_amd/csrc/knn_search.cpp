@@ -278,8 +278,8 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
 
 // Block-scaled int8 candidates (int8 dot4 products, batches of <= kI8MaxQ queries) + exact fp32
 // rerank of K' = 64 + certificate: the bf16 path's chain with the int8 copy's bound.
-int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
-             int64_t* I, hipStream_t st, bool timed, bool first) {
+int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* qnorm, int64_t nq,
+             int k, float* D, int64_t* I, hipStream_t st, bool timed, bool first) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = kB16Cand;
     const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus, ix->i8_wgpcu);
@@ -292,10 +292,19 @@ int i8_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, i
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
     if ((rc = grow_stats(ix, nq, st)) != KNN_OK) return rc;
-    // (the query's int8 codes ix->q8 / q8s / q8r come with qpad from launch_i8_query_prep)
+    // qraw non-NULL: the scan quantises the raw query rows itself and writes qpad / qnorm /
+    // q8r (I8Args::qsrc); otherwise the codes ix->q8 / q8s / q8r came with qpad from
+    // launch_i8_query_prep
     I8Args a{};
     a.codes = ix->x8; a.scales = ix->x8s; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal;
-    a.nblk = ix->nblk8; a.qcodes = ix->q8; a.qscales = ix->q8s; a.qnorm = qnorm; a.nq = (int)nq;
+    a.nblk = ix->nblk8; a.nq = (int)nq;
+    if (qraw) {
+        a.qsrc = qraw; a.d = ix->d; a.dp = ix->dp;
+        a.normalize = ix->metric == KNN_METRIC_COSINE ? 1 : 0;
+        a.qpad = const_cast<float*>(qpad); a.qnorm_out = const_cast<float*>(qnorm); a.qresid = ix->q8r;
+    } else {
+        a.qcodes = ix->q8; a.qscales = ix->q8s; a.qnorm = qnorm;
+    }
     a.km = p.km;
     a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
     a.cand_i = ix->cand_i; a.ncand = p.ncand;
@@ -450,10 +459,16 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         // fused query prep: fp32 padded rows + norms + bf16 + residuals, or for the int8 path
         // the same rows and norms + the two-level int8 codes (one short pass instead of
         // rows_ingest's latency-bound row loop and a second launch)
+        // (the int8 path's prep runs inside its scan unless IMGREC_I8_FUSED_PREP=0: nq_pad = cn)
+        const bool i8_fused = i8 && ix->i8_fused_prep && nq_pad == cn;
         if (i8) {
+            if ((rc = grow(&ix->q8r, &ix->q8r_cap, (size_t)cn)) != KNN_OK) return rc;
+        }
+        if (i8_fused) {
+            q_ready = true;
+        } else if (i8) {
             if ((rc = grow(&ix->q8, &ix->q8_cap, (size_t)cn * ix->nblk8 * 128)) != KNN_OK) return rc;
             if ((rc = grow(&ix->q8s, &ix->q8s_cap, (size_t)cn * ix->nblk8 * 2)) != KNN_OK) return rc;
-            if ((rc = grow(&ix->q8r, &ix->q8r_cap, (size_t)cn)) != KNN_OK) return rc;
             KNN_HIP(launch_i8_query_prep(q + c0 * ix->d, cn, ix->d, ix->dp, nq_pad, normalize,
                                          ix->nblk8, ix->qpad, ix->qnorm, ix->q8, ix->q8s, ix->q8r, st));
             q_ready = true;
@@ -470,7 +485,8 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         float* Dc = D + c0 * k;
         int64_t* Ic = I + c0 * k;
         if (i8 || b16 || split) {
-            rc = i8 ? i8_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, first_cand)
+            rc = i8 ? i8_chunk(ix, i8_fused ? q + c0 * ix->d : nullptr, ix->qpad, ix->qnorm, cn, k,
+                               Dc, Ic, st, true, first_cand)
                : b16 ? b16_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, q_ready, first_cand)
                      : split_chunk(ix, ix->qpad, ix->qnorm, cn, k, Dc, Ic, st, true, first_cand);
             first_cand = false;

@@ -63,6 +63,25 @@ constexpr int kStage = kSA + kSB;
 constexpr int kLPW = (kBM + kBN) / kRPP / kNW;   // DMA pieces per wave per stage
 constexpr int kLDS = 2 * kStage;          // two-slot ring
 constexpr int kDeferQ = 3;                // weight waves issue after this quad of the next stage
+// Measurement builds only (tools/vit_gemm_tiles.py): 1 = the epilogue computed but its stores
+// skipped (data-dependent predicate, never true in practice), 2 = no epilogue at all (one
+// checksum store per tile)
+#ifndef IMGREC_VIT_EPI_EXP
+#define IMGREC_VIT_EPI_EXP 0
+#endif
+// IMGREC_VIT_NT_STORE=1: the output stores non-temporal.  IMGREC_VIT_STORE_WAIT=1: the stage
+// after a full tile's epilogue waits for its own DMA only (vmcnt(16): the 16 output stores of
+// the lane stay in flight), the weight waves issue the DMA they would defer into that stage
+// before the epilogue instead.
+#ifndef IMGREC_VIT_NT_STORE
+#define IMGREC_VIT_NT_STORE 0
+#endif
+#ifndef IMGREC_VIT_STORE_WAIT
+#define IMGREC_VIT_STORE_WAIT 0
+#endif
+#ifndef IMGREC_VIT_STAGGER
+#define IMGREC_VIT_STAGGER 0
+#endif
 static_assert(kBKW == 32 && kCPR == 8 && kRPP == 8 && kRPB == 2, "stage geometry");
 static_assert(kLPW == 8, "pieces go out in two dma4x groups");
 static_assert(kLDS <= 160 * 1024, "LDS budget");
@@ -99,8 +118,20 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
     const int split = rem / G;
     const int qb = qbg * G + rem % G;
     const int ntile = (M + kBM - 1) / kBM;
+#if IMGREC_VIT_STAGGER
+    // a contiguous token range per split, its tile grid shifted by (split mod 4) x 64 rows: the
+    // splits' tile ends (and their output store bursts) fall at four phases instead of one
+    const int per = (ntile + nsplit - 1) / nsplit;
+    const int base = split * per * kBM, end = min(M, base + per * kBM);
+    const int v0 = base - (split & 3) * 64;
+    const int cnt = base < end ? (end - v0 + kBM - 1) / kBM : 0;
+    auto row0_of = [&](int t) { return max(base, v0 + t * kBM); };
+    auto valid_of = [&](int t) { return min(end, v0 + (t + 1) * kBM) - row0_of(t); };
+#else
     const int cnt = split < ntile ? (ntile - split + nsplit - 1) / nsplit : 0;
     auto row0_of = [&](int t) { return (split + t * nsplit) * kBM; };
+    auto valid_of = [&](int t) { return min(kBM, M - row0_of(t)); };
+#endif
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -135,7 +166,7 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
     // issue cursor: stage c_is of tile c_it
     int c_it = 0, c_is = 0;
     const uint32_t* c_tile = isA ? xw + (size_t)row0_of(0) * dw : wblk;
-    int c_valid = isA ? min(kBM, M - row0_of(0)) : kBM;
+    int c_valid = isA ? valid_of(0) : kBM;
     auto issue = [&](int g) __attribute__((always_inline)) {
         const uint32_t* src = c_tile + c_is * kBKW;
         const uint32_t dst = smem0 + (uint32_t)((g & 1) * kStage) + pdst;
@@ -163,7 +194,7 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
             ++c_it;
             if (isA && c_it < cnt) {
                 c_tile = xw + (size_t)row0_of(c_it) * dw;
-                c_valid = min(kBM, M - row0_of(c_it));
+                c_valid = valid_of(c_it);
             }
         }
     };
@@ -207,6 +238,7 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
         read_a(smem, 0, fa[0]);
         read_b(smem, 0, fb[0]);
     }
+    bool prev_full = false;            // the previous tile's epilogue issued all 16 stores
     for (int t = 0; t < cnt; ++t) {
         f32x4 acc[kRB][2];
 #pragma unroll
@@ -214,7 +246,7 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
 #pragma unroll
             for (int h = 0; h < 2; ++h) acc[rb][h] = (f32x4){0.f, 0.f, 0.f, 0.f};
         const int row0 = row0_of(t);
-        const int valid = min(kBM, M - row0);
+        const int valid = valid_of(t);
         // live quad rows (64 tokens each): a partial last tile runs the MFMAs of its live rows only
         const int nlive = (valid + 63) >> 6;
         auto stage_loop = [&](auto nr_tag) __attribute__((always_inline)) {
@@ -249,7 +281,10 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                if (IMGREC_VIT_STORE_WAIT && s == 0 && prev_full)
+                    asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_sched_barrier(0);
                 barrier_lds();
                 __builtin_amdgcn_sched_barrier(0);
@@ -259,7 +294,9 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
                     read_b(nb, 0, fb[0]);
                 }
                 if (g + 2 < total) {
-                    if (isA) issue(g + 2);
+                    // (IMGREC_VIT_STORE_WAIT: a tile's last stage issues for the weight waves too,
+                    // so the next tile's first stage waits on no DMA issued after the stores)
+                    if (isA || (IMGREC_VIT_STORE_WAIT && s + 1 == nst)) issue(g + 2);
                     else pend = g + 2;
                 }
                 mfma_quad(acc, fa[1], fb[1], 4 + NR - 1);
@@ -276,6 +313,14 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
         // the 16-lane form): even quarters end with h = 0's features 4 lq .. 4 lq + 7, odd ones with
         // h = 1's 16 + 4 (lq - 1) .. + 7 — half the store instructions of 8-B stores, whose issue
         // rate, not HBM, sets this tail
+#if IMGREC_VIT_EPI_EXP == 2
+        {
+            float cs = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < kRB; ++rb) cs += acc[rb][0][0] + acc[rb][1][3];
+            if (__float_as_uint(cs) == 0x7f812345u) y[lane] = 1;
+        }
+#else
 #pragma unroll
         for (int rb = 0; rb < kRB; ++rb) {
             const int tok = row0 + 16 * rb + lc;
@@ -294,10 +339,23 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
                 o[0][d] = r[0];
                 o[1][d] = r[1];
             }
-            if (tok < M)
-                *reinterpret_cast<uint4*>(y + (size_t)tok * N + fcol + ((lq & 1) ? 12 : 0)) =
-                    make_uint4(o[0][0], o[0][1], o[1][0], o[1][1]);
+#if IMGREC_VIT_EPI_EXP == 1
+            if ((o[0][0] ^ o[1][1]) == 0x12345678u && 16 * rb + lc < valid)
+#else
+            if (16 * rb + lc < valid)
+#endif
+            {
+                uint4* dst = reinterpret_cast<uint4*>(y + (size_t)tok * N + fcol + ((lq & 1) ? 12 : 0));
+#if IMGREC_VIT_NT_STORE
+                __builtin_nontemporal_store((u32x4){o[0][0], o[0][1], o[1][0], o[1][1]},
+                                            reinterpret_cast<u32x4*>(dst));
+#else
+                *dst = make_uint4(o[0][0], o[0][1], o[1][0], o[1][1]);
+#endif
+            }
         }
+#endif
+        prev_full = valid == kBM;
         if (g < total) {
             read_a(smem + (g & 1) * kStage, 0, fa[0]);
             read_b(smem + (g & 1) * kStage, 0, fb[0]);

@@ -242,3 +242,34 @@ def test_i8_mode_refused_outside_its_dimensions(faiss):
         with pytest.raises(RuntimeError):
             idx.search_mode = "i8"
         assert idx.search_mode == "auto"
+
+
+@pytest.mark.parametrize("d", [64, 100, 300, 1968, 4096])
+@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
+def test_i8_fused_query_prep_matches_its_own_launch(faiss, monkeypatch, d, metric):
+    """The scan derives the two-level query codes, |q|^2, |q - q~| and the padded fp32 rows itself
+    (I8Args::qsrc, round 5) with i8_query_prep_kernel's arithmetic: every returned bit equals the
+    separate prep launch's (IMGREC_I8_FUSED_PREP=0) at widths that are not a multiple of 4, 8, 64
+    (d = 100, 300) or span 1-64 blocks, for 1-8 queries (one wave quantising two of them at 5-8)
+    and every metric (cosine: the in-scan normalisation)."""
+    xb = mixture(5003, d, centres=40, seed=d + 7)
+    xq = mixture(8, d, centres=40, seed=d + 8)
+    idx = {}
+    for name, env in (("fused", None), ("separate", "0")):
+        if env is not None:
+            monkeypatch.setenv("IMGREC_I8_FUSED_PREP", env)
+        idx[name] = _index(faiss, d, metric)          # (the knob is read at index creation)
+        monkeypatch.delenv("IMGREC_I8_FUSED_PREP", raising=False)
+        idx[name].add(xb)
+        idx[name].search_mode = "i8"
+    for nq in (1, 3, 5, 8):
+        q = np.ascontiguousarray(xq[:nq])
+        D0, I0 = idx["separate"].search(q, 10)
+        D1, I1 = idx["fused"].search(q, 10)
+        assert _lib().knn_last_path(idx["fused"].handle) == 3
+        assert np.array_equal(I1, I0), (nq, np.argwhere(I1 != I0)[:5])
+        assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), nq
+        _stats(idx["fused"], nq)
+    # (at d >= 1024 the mixture's neighbours crowd inside the rigorous window, as in
+    # test_i8_l2_shapes: the tight check there, the identity with the separate launch here)
+    check_knn(D1, I1, xb, xq, 10, metric, min_exact_frac=0.5 if d < 1024 else 0.25)

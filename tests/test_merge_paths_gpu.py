@@ -7,8 +7,9 @@ merge route and however many per-split lists the scan writes, the certified top-
 with the same exact fp32 keys (the rerank's key form does not depend on the route), so these
 tests compare the default index against indexes created with IMGREC_MERGE_FUSE=0 (both levels
 as their own launches) and =1 (level 1 launched, level 2 in the rerank), IMGREC_I8_WGPCU=1 / 5 (256 / 1280 lists per query against the default 512 or
-768: 4 / 20 level-1 groups) and IMGREC_CHANCE_SKIP=0 (every query through the first rerank, none
-sent straight to the second chance by its band)
+768: 4 / 20 level-1 groups), IMGREC_CHANCE_SKIP=0 (every query through the first rerank, none
+sent straight to the second chance by its band) and IMGREC_I8_FUSED_PREP=0 (the int8 query codes
+from their own launch instead of inside the scan)
 bit for bit, and the default against the float64 oracle (tests/knn_check.py).  The config-2
 distribution (bench.py's 1M x 768 rows) makes most single queries take the second
 chance, so the tail's hand-offs run under every route.
@@ -50,7 +51,8 @@ def _index(xb, env, monkeypatch):
 
 VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "level2only": {"IMGREC_MERGE_FUSE": "1"},
             "wgpcu1": {"IMGREC_I8_WGPCU": "1"},
-            "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"}}
+            "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"},
+            "separate_prep": {"IMGREC_I8_FUSED_PREP": "0"}}
 
 
 @pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257])

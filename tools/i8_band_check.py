@@ -1,22 +1,26 @@
 #!/usr/bin/env python3
 """numpy check behind the int8 small-batch path (DESIGN.md "Small batches"): residual norm R of
 the block-scaled int8 copy and the number of rows inside the certificate band per query, over the
-whole 1M x 1968 bench corpus (bench.py generator on the CPU).  CPU only, ~3 min, ~20 GB RAM."""
+whole 1M x 1968 bench corpus (bench.py generator on the CPU).  CPU only, ~3 min, ~20 GB RAM.
+CFG=2 runs bench config 2 (1M x 768) instead; VARIANTS=blk64 limits the block sizes."""
+import os
 import numpy as np, torch, sys, time
 sys.path.insert(0, '/root/repo')
 import bench
 torch.set_num_threads(8)
-cfg = bench.CONFIGS[3]
+CFGN = int(os.environ.get("CFG", "3"))
+cfg = bench.CONFIGS[CFGN]
 dev = 'cpu'
-cent = bench.make_centres(torch, cfg, dev, 3)
+cent = bench.make_centres(torch, cfg, dev, CFGN)
 N = 1_000_000
-xq = bench.gen_queries(torch, cfg, cent, 32, dev, 3).numpy().astype(np.float64)
+xq = bench.gen_queries(torch, cfg, cent, 32, dev, CFGN).numpy().astype(np.float64)
 D = xq.shape[1]
 res = {}
-variants = [("blk64", 64), ("blk32", 32)]
+variants = [v for v in [("blk64", 64), ("blk32", 32)]
+            if v[0] in os.environ.get("VARIANTS", "blk64,blk32").split(",")]
 EX = []; AP = {v: [] for v, _ in variants}; RR = {v: [] for v, _ in variants}
 t0 = time.time()
-for blk in bench.gen_rows(torch, cfg, cent, 0, N, dev, 3):
+for blk in bench.gen_rows(torch, cfg, cent, 0, N, dev, CFGN):
     xb = blk.numpy().astype(np.float64)
     n = xb.shape[0]
     EX.append((xq**2).sum(1)[:, None] + (xb**2).sum(1)[None] - 2 * xq @ xb.T)

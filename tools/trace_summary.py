@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Per-kernel durations and gaps of the last search step in a rocprofv3 kernel trace: the step is
-the run of kernels ending at the last `knn` kernel, starting at the last query-prep kernel."""
+the run of kernels ending at the last `knn` kernel, starting at the last query-prep kernel (or,
+when the query prep runs inside the int8 scan, at the last knn_i8_scan_kernel)."""
 import csv, sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 names = [r["Kernel_Name"] for r in rows]
-last = max(i for i, n in enumerate(names) if "prep" in n or "query" in n)
+starts = [i for i, n in enumerate(names) if "prep" in n or "query" in n]
+last = max(starts) if starts else max(i for i, n in enumerate(names) if "knn_i8_scan" in n)
 # the step starts at the last query-prep kernel that begins a chain (walk back over i8 query)
 start = last
 while start > 0 and ("prep" in names[start - 1] or "query" in names[start - 1]):
