@@ -281,6 +281,8 @@ int create_single(int d, int metric, int device, knn_index** out) {
     }
     if (const char* e = test_knob("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
     if (const char* e = test_knob("IMGREC_I8_FUSED_PREP")) ix->i8_fused_prep = *e != '0';
+    if (const char* e = test_knob("IMGREC_RERANK_P1")) ix->rerank_p1k = *e != '0';
+    if (const char* e = test_knob("IMGREC_MERGE_SINGLE")) ix->merge_single = *e != '0';
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ix->fence, hipEventDisableTiming) != hipSuccess) {
         if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -666,7 +668,7 @@ int knn_plan(const knn_index_t* cix, int64_t nq, int k, int* tr, int* tq, int* s
     if (!cix || !tr || !tq || !splits || !wgs) KNN_FAIL(KNN_EINVAL, "NULL argument");
     const knn_index* ix = cix->multi ? multi_shard(cix, 0) : cix;
     const int64_t cn = std::min(nq, kQueryChunk);
-    const Plan p = use_i8(ix, cn, k) ? make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu)
+    const Plan p = use_i8(ix, cn, k) ? make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu, ix->nblk8)
                  : use_b16(ix, cn, k) ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                  : use_split(ix, cn, k) ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                                         : make_plan(ix->ntotal, cn, k, ix->cus);
@@ -683,7 +685,7 @@ int knn_plan_kernel(const knn_index_t* cix, int64_t nq, int k, char* name, int c
     const int64_t cn = std::min(nq, kQueryChunk);
     const int l2 = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     if (use_i8(ix, cn, k)) {
-        const Plan p = make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu);
+        const Plan p = make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu, ix->nblk8);
         std::snprintf(name, cap, "knn_i8_scan_kernel<%d, %d, %d>", cn <= 2 ? (int)cn : (cn <= 4 ? 4 : 8), p.km,
                       (ix->nblk8 + 15) / 16);
     } else if (use_b16(ix, cn, k)) {

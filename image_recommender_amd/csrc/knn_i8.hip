@@ -44,9 +44,7 @@ constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA pi
 #define IMGREC_I8_NT 1
 #endif
 constexpr bool kNtCodes = IMGREC_I8_NT != 0;   // non-temporal code loads in the scan
-#ifndef IMGREC_I8_PRELOAD
-#define IMGREC_I8_PRELOAD 1
-#endif
+
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -424,13 +422,8 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
             if (__any(kv != INFINITY)) insert_mono<KM>(kd, ki, kv, G.row[h]);
         }
     };
-    // the first group's code loads go out before the query side is ready (IMGREC_I8_PRELOAD):
-    // their HBM round trip overlaps the fused prep's quantising or the codes' copy into LDS
     Grp A, B;
     int li = wave;
-    // (only where the group's codes are <= 32 registers: holding 64 across the prep spills)
-    constexpr bool kPre = IMGREC_I8_PRELOAD && H * NBI <= 2 && NQ <= 4;
-    if (kPre && li < cnt) load(li, A);
     __shared__ float s_qn[NQ];
     if (qsrc) {
         // Fused query prep (I8Args::qsrc): wave w derives queries w, w + 4 from the raw rows with
@@ -548,7 +541,9 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     for (int q = 0; q < NQ; ++q)      // (uniform: scalar registers, as the kernel-argument loads were)
         qn[q] = (l2 && q < nq) ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_qn[q]))) : 0.f;
 
-    if (!kPre && li < cnt) load(li, A);
+    // (the first group's loads issued before the query prep instead measured the same:
+    // profiles/r05/nq1/preload/)
+    if (li < cnt) load(li, A);
     while (li < cnt) {
         if (li + kWaves < cnt) load(li + kWaves, B);
         process(A);

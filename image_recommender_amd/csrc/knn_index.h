@@ -87,7 +87,7 @@ float b16_acc_coef(int dpb);
 constexpr int kI8MaxQ = 8;
 float i8_acc_coef(int nblk);
 // wgpcu: int8 scan workgroups per CU (the split count is CUs x wgpcu); 0 = by batch size
-Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus, int wgpcu);
+Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus, int wgpcu, int nblk);
 constexpr int kI8WGPCUDefault = 0;
 constexpr int kB16Cand = 64;                   // K': candidates the bf16 pass hands to the rerank
 int b16_km(int k);
@@ -102,6 +102,8 @@ struct knn_index {
     int i8_wgpcu = imgrec::kI8WGPCUDefault;
     bool merge_fuse = true;
     bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
+    bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
+    bool rerank_p1k = true;     // large batches rerank k rows first (IMGREC_RERANK_P1=0: 16)
     bool i8_fused_prep = true;  // int8 query prep inside the scan (IMGREC_I8_FUSED_PREP=0: own launch)
     bool merge_fuse1 = true;    // IMGREC_MERGE_FUSE=1: only level 2 in the rerank (0: neither)
     int64_t ntotal = 0, cap = 0, id_offset = 0;

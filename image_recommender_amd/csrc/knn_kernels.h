@@ -79,6 +79,12 @@ struct RerankArgs {
     // kRerankWaves) per-split lists of 16 are selected by the rerank's waves (one group of 64 lists
     // a wave, l1_G = groups); no merge launch at all
     int l0_lists = 0;
+    // s_lists > 0: ONE merge level, in this kernel — the raw_lists (= s_lists <= 64) per-split
+    // lists of raw_km <= 16 entries are selected by the whole workgroup (large batches' single
+    // level; no merge launch)
+    int s_lists = 0;
+    int p1 = 0;                 // first-phase rerank size (0 = kRerankWaves x kRerankRows = 16);
+                                // large batches use k: their rerank is bound by row bytes
     int chance_skip = 0;        // queue a query whose band certainly-ish exceeds K' straight to the
                                 // second chance (no first-pass row reads); needs raw_d
     float* D;

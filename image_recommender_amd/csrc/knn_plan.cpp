@@ -96,8 +96,12 @@ float i8_acc_coef(int nblk) {
 // Workgroups per CU of the int8 scan: 2 for one or two queries (fewer lists for the merge, and
 // the scan itself no slower: cfg2 one query 0.187 -> 0.182 ms), 3 from four queries on (cfg2 at
 // nq = 8: 0.406 ms with 2, 0.358 with 3) — profiles/r04/i8_wgpcu/.
-Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus, int wgpcu) {
-    const int kI8WGPCU = wgpcu > 0 ? wgpcu : (nq <= 2 ? 2 : 3);
+// Workgroups per CU of the int8 scan: 3 from three queries, 2 for one or two (fewer lists for the
+// merge, no slower a scan: profiles/r04/i8_wgpcu/), 1 for ONE query on rows of >= 24 blocks (the
+// 1M x 1968 scan 0.311 -> 0.308 ms and the search 3 us shorter on two boxes, while 1M x 768 rows
+// lose 28 us with one: sweep_nq1_b.txt).  IMGREC_I8_WGPCU overrides.
+Plan make_i8_plan(int64_t ntotal, int64_t nq, int k, int cus, int wgpcu, int nblk) {
+    const int kI8WGPCU = wgpcu > 0 ? wgpcu : (nq == 1 && nblk >= 24 ? 1 : nq <= 2 ? 2 : 3);
     Plan p{};
     p.km = b16_km(k);
     p.wr = 1;

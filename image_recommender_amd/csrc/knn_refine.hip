@@ -230,7 +230,7 @@ rerank_certify_kernel(const RerankArgs a) {
     // one list) and the kc smallest land at their ranks — for this kernel (LDS) and the second
     // chance (global).  (The wave threshold select of cand_merge_lane_kernel took ~10 us here:
     // 32 dependent wave-sum steps in one wave while seven waited.)
-    const bool fused = a.l1_G > 0;
+    const bool fused = a.l1_G > 0 || a.s_lists > 0;
     __shared__ float s_mkey[64];
     __shared__ int64_t s_mlab[64];
     __shared__ __attribute__((aligned(16))) uint64_t s_ent[kRerankWaves * 64];
@@ -240,7 +240,106 @@ rerank_certify_kernel(const RerankArgs a) {
     // into s_ent[16 w ..] and the group's floor (the last key of its full lists) into s_gfl[w]
     __shared__ uint64_t s_sel[kRerankWaves][64 + 256];
     __shared__ float s_gfl[kRerankWaves];
-    if (fused) {
+    if (fused && a.s_lists > 0) {
+        // RerankArgs::s_lists: the single-level merge (<= 64 lists of raw_km <= 16 entries: the
+        // large batches' per-split lists) by the whole workgroup.  Thread t holds entries t and
+        // t + 512; U = the kc-th smallest of the lists' first two entries bounds the answer (kc
+        // distinct entries are <= it), the entries <= U are compacted in LDS and each ranked
+        // against the others; the kc best land at their ranks (LDS for the rerank, global for the
+        // second chance) and the floor is the smallest last key of the full lists — the same
+        // result as cand_merge_lane_kernel's wave select, without its launch or the candidates'
+        // round trip through global memory.
+        constexpr uint64_t kEmpty = ~0ull;
+        constexpr int NT = kRerankWaves * 64;
+        const int t = threadIdx.x, KIN = a.raw_km, L = a.s_lists, E = L * KIN;
+        const float* rd = a.raw_d + q * a.raw_stride_q;
+        const int64_t* ri = a.raw_i + q * a.raw_stride_q;
+        uint64_t* lead = &s_sel[0][0];                       // 2 L leading entries
+        uint64_t* surv = &s_sel[0][0] + 128;                 // survivors (<= E - 128 + 128)
+        __shared__ uint64_t s_U;
+        __shared__ int s_cnt;
+        uint64_t v[2] = {kEmpty, kEmpty};
+        float fl = INFINITY;
+        int nlead = 0, nval = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int e = t + NT * h;
+            if (e < E) {
+                const int64_t lb = ri[e];
+                const float kv = rd[e];
+                if (lb >= 0) {
+                    v[h] = ((uint64_t)key_bits_ordered(kv) << 32) | (uint32_t)(lb - id_offset);
+                    ++nval;
+                    if (e % KIN == KIN - 1) fl = fminf(fl, kv);  // a full list: its last key
+                }
+                const int p = e % KIN;
+                if (p < 2) {
+                    lead[(e / KIN) * 2 + p] = v[h];
+                    nlead += v[h] != kEmpty ? 1 : 0;
+                }
+            }
+        }
+        if (t == 0) s_cnt = 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) fl = fminf(fl, __shfl_xor(fl, off, 64));
+        if (lane == 0) s_gfl[wave] = fl;
+        int nlead_all = 0, nval_all = 0;
+        {                                                    // (its barrier also publishes lead[])
+            __shared__ int s_nl[kRerankWaves], s_nv[kRerankWaves];
+            const int wl = wave_sum_i32(nlead), wv = wave_sum_i32(nval);
+            if (lane == 0) { s_nl[wave] = wl; s_nv[wave] = wv; }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < kRerankWaves; ++i) { nlead_all += s_nl[i]; nval_all += s_nv[i]; }
+        }
+        const int K = min(kc, nval_all);
+        if (nlead_all >= kc) {
+            // exactly one valid leading entry has rank kc - 1 among the 2 L (distinct entries)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = t + NT * h;
+                if (e < E && e % KIN < 2 && v[h] != kEmpty) {
+                    int r = 0;
+                    for (int j = 0; j < 2 * L; ++j) r += lead[j] < v[h] ? 1 : 0;
+                    if (r == kc - 1) s_U = v[h];
+                }
+            }
+        } else if (t == 0) {
+            s_U = kEmpty - 1;                                // fewer than kc leads: all compete
+        }
+        __syncthreads();
+        const uint64_t U = s_U;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (v[h] <= U) surv[atomicAdd(&s_cnt, 1)] = v[h];
+        __syncthreads();
+        const int C = s_cnt;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (v[h] <= U) {
+                int r = 0;
+                for (int j = 0; j < C; ++j) r += surv[j] < v[h] ? 1 : 0;
+                if (r < K) {
+                    const float kv = key_from_ordered((uint32_t)(v[h] >> 32));
+                    const int64_t lb = (int64_t)(uint32_t)v[h] + id_offset;
+                    s_mkey[r] = kv; s_mlab[r] = lb;
+                    a.cd[q * kc + r] = kv; a.ci[q * kc + r] = lb;
+                }
+            }
+        }
+        if (t >= K && t < kc) {
+            s_mkey[t] = FLT_MAX; s_mlab[t] = -1;
+            a.cd[q * kc + t] = FLT_MAX; a.ci[q * kc + t] = -1;
+        }
+        if (wave == 0) {
+            float f = lane < kRerankWaves ? s_gfl[lane] : INFINITY;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) f = fminf(f, __shfl_xor(f, off, 64));
+            if (lane == 0) { s_floor = f; a.floor[q] = f; }
+        }
+        __syncthreads();
+        RR_STAMP(3);
+    } else if (fused) {
         constexpr uint64_t kEmpty = ~0ull;
         const int t = threadIdx.x, G = a.l1_G, E = 16 * G;
         uint64_t mine = kEmpty;
@@ -412,7 +511,11 @@ rerank_certify_kernel(const RerankArgs a) {
     // (any other has exact key > s1 + E_f(s1): v - E_a(v) is increasing, and a truncated key is
     // below the approximate key it stands for).  The refined prefix replaces a_k's twice-bounded
     // limit; its first candidate left out passes the certificate by construction.
-    constexpr int P1 = kRerankWaves * kRerankRows;
+    // P1 = RerankArgs::p1 (k for large batches: the first k candidates usually ARE the answer
+    // and their max exact key already cuts the rest, so the 16 - k extra rows a 16-row first
+    // phase reads are bytes a throughput-bound batch pays for; small batches keep 16 — one round
+    // of row loads — since a second phase is a dependent round trip there)
+    const int P1 = a.p1 > 0 ? a.p1 : kRerankWaves * kRerankRows;
     const int m1 = min(m, P1);
     rerank_range(0, m1, std::integral_constant<int, kRerankRows>{});
     __syncthreads();

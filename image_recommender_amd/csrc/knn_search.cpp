@@ -143,6 +143,9 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     // queue up in the tail; at 1024 queries the A/B was within the +-15 us noise of the step,
     // profiles/r04/chance_skip/ab_env_nq1024*.txt, so large batches keep the round-3 route)
     r.chance_skip = ix->chance_skip && r.raw_d && nq <= ix->cus ? 1 : 0;
+    // first rerank phase of k rows for batches past one rerank workgroup per CU
+    // (IMGREC_RERANK_P1: 0 keeps 16 everywhere, for A/B)
+    r.p1 = ix->rerank_p1k && nq > ix->cus ? k : 0;
     KNN_HIP(launch_rerank_certify(r, st));
     TailArgs t{};
     t.r = r;
@@ -192,6 +195,16 @@ bool fuse_merge_level2(const knn_index* ix, int64_t nq) {
 bool fuse_merge_level1(const knn_index* ix, int64_t nq, int nlists, int km) {
     return fuse_merge_level2(ix, nq) && ix->merge_fuse1 && km == 16 && nlists > 64 &&
            nlists <= 64 * kRerankWavesHost;
+}
+
+// A single-level merge (<= 64 per-split lists of <= 16: the 256 x 256 kernel's 64 lists of 8 / 10)
+// inside the rerank workgroup (RerankArgs::s_lists): no merge launch and no round trip of the K'
+// candidates through global memory.  Measured at 1024 queries it saves nothing — the 10.8-us
+// launch comes back as rerank workgroups that hold their CU longer (125k rows 0.4815 vs 0.4846 ms
+// per step, cfg3 3.181 vs 3.189, two runs each on one box: profiles/r05/merge_rerank_ab/) — so it
+// is opt-in: IMGREC_MERGE_SINGLE=1 at index creation.
+bool fuse_merge_single(const knn_index* ix, int nlists, int km) {
+    return ix->merge_single && nlists <= 64 && km <= 16;
 }
 
 // Sibling lockstep of the 256 x 256 bf16 kernel (TileArgs::sync): IMGREC_B16W_SYNC_LAG = the
@@ -254,15 +267,17 @@ int b16_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, 
         if ((rc = grow(&ix->mws_f, &ix->mws_f_cap, (size_t)nq * ngrp)) != KNN_OK) return rc;
     }
     int l1G = 0;
-    const bool l0 = fuse_merge_level1(ix, nq, nlists, km);
+    const bool single = fuse_merge_single(ix, nlists, km);
+    const bool l0 = !single && fuse_merge_level1(ix, nq, nlists, km);
     if (l0) l1G = (nlists + 63) / 64;
-    else
+    else if (!single)
         KNN_HIP(launch_merge_candidates(ix->cand_d, ix->cand_i, nq, nlists, km, p.ncand, km, kc,
                                         ix->id_offset, ix->cand2_d, ix->cand2_i, ix->floor,
                                         ix->mws_d, ix->mws_i, ix->mws_f, st,
                                         fuse_merge_level2(ix, nq) ? &l1G : nullptr));
     RerankArgs r{};
     r.mode = kModeBF16;
+    if (single) r.s_lists = nlists;
     r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
     r.xn_max = ix->xn_max; r.id_offset = ix->id_offset; r.cd = ix->cand2_d; r.ci = ix->cand2_i;
     r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = b16_acc_coef(ix->dpb);
@@ -282,7 +297,7 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
              int k, float* D, int64_t* I, hipStream_t st, bool timed, bool first) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = kB16Cand;
-    const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus, ix->i8_wgpcu);
+    const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus, ix->i8_wgpcu, ix->nblk8);
     int rc;
     if ((rc = ensure_i8(ix, st)) != KNN_OK) return rc;
     if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
@@ -402,10 +417,12 @@ bool use_b16(const knn_index* ix, int64_t nq, int k) {
 // VALU-bound and still faster than the bf16 pass; one query on 1000-65536 rows 0.05-0.075 ms
 // against the exact kernel's 0.18-0.22, profiles/r03/small_corpora/)
 // A row's 16-lane group in the scan has one lane per 64-element block, so narrow rows leave most
-// lanes idle (d = 128: 2 of 16) and the scan stops being HBM-bound: below kI8MinBlocks blocks
-// AUTO takes the int8 path only while the copy is small enough (<= 64 MB, ~10 us of streaming)
-// for the fixed costs to decide (round 3 measured one query on 1M x 128 rows: int8 0.223 ms,
-// bf16 0.162, with the then-padded 1-KiB rows; profiles/r03/small_corpora/small_d.jsonl).
+// lanes idle (d = 128: 2 of 16).  One or two queries stay HBM-bound at every width since the
+// rows are compact (round 4): one query on 1M rows, int8 against bf16, 0.133 / 0.143 ms at
+// d = 64, 0.134 / 0.154 at 128, 0.137 / 0.183 at 256, 0.140 / 0.221 at 384, 0.140 / 0.247 at 512
+// (profiles/r05/small_d/), so they take the int8 path at any width.  Larger batches multiply the
+// dot products per byte: below kI8MinBlocks blocks they take it only while the copy is small
+// enough (<= 64 MB, ~10 us of streaming) for the fixed costs to decide.
 constexpr int kI8AutoQ = 8;
 constexpr int kI8MinBlocks = 8;
 constexpr int64_t kI8SmallCopyBytes = 64ll << 20;
@@ -414,7 +431,7 @@ bool use_i8(const knn_index* ix, int64_t nq, int k) {
     if (ix->mode == KNN_SEARCH_I8) return true;
     if (ix->mode != KNN_SEARCH_AUTO || nq > kI8AutoQ) return false;
     const int64_t i8_row = i8_row_bytes(ix->nblk8) + 4 * ix->nblk8;
-    return !ix->b16_ok || ix->nblk8 >= kI8MinBlocks || ix->ntotal * i8_row <= kI8SmallCopyBytes;
+    return !ix->b16_ok || nq <= 2 || ix->nblk8 >= kI8MinBlocks || ix->ntotal * i8_row <= kI8SmallCopyBytes;
 }
 
 bool use_split(const knn_index* ix, int64_t nq, int k) {
@@ -446,7 +463,7 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         const bool b16 = !i8 && use_b16(ix, cn, k);
         const bool split = !i8 && !b16 && use_split(ix, cn, k);
         // padding: the query tile of the plan this chunk will run (and the exact re-run's 32)
-        const Plan p = i8 ? make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu)
+        const Plan p = i8 ? make_i8_plan(ix->ntotal, cn, k, ix->cus, ix->i8_wgpcu, ix->nblk8)
                      : b16 ? make_b16_plan(ix->ntotal, cn, k, ix->cus, ix->dpb)
                      : split ? make_split_plan(ix->ntotal, cn, split_kc(k), ix->cus)
                              : make_plan(ix->ntotal, cn, k, ix->cus);

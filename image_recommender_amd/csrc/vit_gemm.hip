@@ -69,18 +69,19 @@ constexpr int kDeferQ = 3;                // weight waves issue after this quad 
 #ifndef IMGREC_VIT_EPI_EXP
 #define IMGREC_VIT_EPI_EXP 0
 #endif
-// IMGREC_VIT_NT_STORE=1: the output stores non-temporal.  IMGREC_VIT_STORE_WAIT=1: the stage
-// after a full tile's epilogue waits for its own DMA only (vmcnt(16): the 16 output stores of
-// the lane stay in flight), the weight waves issue the DMA they would defer into that stage
-// before the epilogue instead.
+// The output stores are non-temporal (IMGREC_VIT_NT_STORE, default on) and the stage after a
+// full tile's epilogue waits for its own DMA only (IMGREC_VIT_STORE_WAIT, default on: vmcnt(16) —
+// the lane's 16 output stores stay in flight; the weight waves issue the DMA they would defer into
+// that stage before the epilogue instead).  Every CU ends its tiles at the same moment, so a tile
+// end is a 32 MB burst of output stores; waiting for it at the next stage and leaving the lines
+// dirty in the L2 the operand stream runs through cost up to a third of the K = 768 GEMMs
+// (stores skipped: qkv 0.364 -> 0.271 ms).  Measured at batch 512 (profiles/r05/vit_gemm/):
+// qkv 0.357 -> 0.315 ms, proj 0.138 -> 0.110, fc1 + GELU 0.494 -> 0.456, fc2 0.416 -> 0.407.
 #ifndef IMGREC_VIT_NT_STORE
-#define IMGREC_VIT_NT_STORE 0
+#define IMGREC_VIT_NT_STORE 1
 #endif
 #ifndef IMGREC_VIT_STORE_WAIT
-#define IMGREC_VIT_STORE_WAIT 0
-#endif
-#ifndef IMGREC_VIT_STAGGER
-#define IMGREC_VIT_STAGGER 0
+#define IMGREC_VIT_STORE_WAIT 1
 #endif
 static_assert(kBKW == 32 && kCPR == 8 && kRPP == 8 && kRPB == 2, "stage geometry");
 static_assert(kLPW == 8, "pieces go out in two dma4x groups");
@@ -118,20 +119,9 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
     const int split = rem / G;
     const int qb = qbg * G + rem % G;
     const int ntile = (M + kBM - 1) / kBM;
-#if IMGREC_VIT_STAGGER
-    // a contiguous token range per split, its tile grid shifted by (split mod 4) x 64 rows: the
-    // splits' tile ends (and their output store bursts) fall at four phases instead of one
-    const int per = (ntile + nsplit - 1) / nsplit;
-    const int base = split * per * kBM, end = min(M, base + per * kBM);
-    const int v0 = base - (split & 3) * 64;
-    const int cnt = base < end ? (end - v0 + kBM - 1) / kBM : 0;
-    auto row0_of = [&](int t) { return max(base, v0 + t * kBM); };
-    auto valid_of = [&](int t) { return min(end, v0 + (t + 1) * kBM) - row0_of(t); };
-#else
     const int cnt = split < ntile ? (ntile - split + nsplit - 1) / nsplit : 0;
     auto row0_of = [&](int t) { return (split + t * nsplit) * kBM; };
     auto valid_of = [&](int t) { return min(kBM, M - row0_of(t)); };
-#endif
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -105,7 +105,8 @@ def test_i8_concat_layout_self_query(faiss):
 
 def test_i8_auto_picks_int8_for_single_queries(faiss):
     """AUTO: one to eight queries take the int8 path, nine the bf16 path; below 8 blocks per row
-    (d <= 448: most of a row's 16 scan lanes idle) only while the int8 copy is small."""
+    (d <= 448: most of a row's 16 scan lanes idle) one or two queries always (HBM-bound at every
+    width, round 5), three to eight only while the int8 copy is small."""
     d = 1024
     xb = mixture(140000, d, centres=200, seed=3)
     xq = mixture(9, d, centres=200, seed=4)
@@ -124,10 +125,13 @@ def test_i8_auto_picks_int8_for_single_queries(faiss):
     narrow.add(xn[:30000])                                   # 8 MB int8 copy: int8
     narrow.search(xn[:1], 10)
     assert _lib().knn_last_path(narrow.handle) == 3
-    narrow.add(xn[30000:])                                   # 71 MB: bf16
+    narrow.add(xn[30000:])                                   # 71 MB: bf16 from 3 queries
     D, I = narrow.search(xn[:1], 10)
-    assert _lib().knn_last_path(narrow.handle) == 2
+    assert _lib().knn_last_path(narrow.handle) == 3
     assert I[0, 0] == 0
+    D, I = narrow.search(xn[:3], 10)
+    assert _lib().knn_last_path(narrow.handle) == 2
+    assert (I[:, 0] == np.arange(3)).all()
 
 
 def test_i8_rows_added_after_the_copy_exists(faiss):

@@ -9,7 +9,9 @@ tests compare the default index against indexes created with IMGREC_MERGE_FUSE=0
 as their own launches) and =1 (level 1 launched, level 2 in the rerank), IMGREC_I8_WGPCU=1 / 5 (256 / 1280 lists per query against the default 512 or
 768: 4 / 20 level-1 groups), IMGREC_CHANCE_SKIP=0 (every query through the first rerank, none
 sent straight to the second chance by its band) and IMGREC_I8_FUSED_PREP=0 (the int8 query codes
-from their own launch instead of inside the scan)
+from their own launch instead of inside the scan) and IMGREC_RERANK_P1=0 (a 16-row first rerank
+phase for every batch instead of k rows past one rerank workgroup per CU) and
+IMGREC_MERGE_SINGLE=1 (the single-level merge of <= 64 lists inside the rerank workgroup)
 bit for bit, and the default against the float64 oracle (tests/knn_check.py).  The config-2
 distribution (bench.py's 1M x 768 rows) makes most single queries take the second
 chance, so the tail's hand-offs run under every route.
@@ -52,10 +54,11 @@ def _index(xb, env, monkeypatch):
 VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "level2only": {"IMGREC_MERGE_FUSE": "1"},
             "wgpcu1": {"IMGREC_I8_WGPCU": "1"},
             "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"},
-            "separate_prep": {"IMGREC_I8_FUSED_PREP": "0"}}
+            "separate_prep": {"IMGREC_I8_FUSED_PREP": "0"}, "rerank_p1_16": {"IMGREC_RERANK_P1": "0"},
+            "single_fused": {"IMGREC_MERGE_SINGLE": "1"}}
 
 
-@pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257])
+@pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257, 1024])
 def test_routes_return_identical_bits(corpus, monkeypatch, nq):
     """nq 1-8: the int8 path (split counts 1-5 per CU, fused or separate level 2); nq = 16: the
     bf16 path's small-batch tile with the fused or separate level 2; 256 / 257: the last batch
