@@ -195,7 +195,7 @@ query_prep_b16_kernel(const float* __restrict__ src, int64_t n, int d, int dp, i
 // query with the rows (any dp).
 // A query whose certificate fails goes to the second-chance queue (a.raw_d set: stats[3] counts
 // it) or straight to the exact re-run list (stats[0]).
-template <int IT>
+template <int IT, bool SL>
 __global__ void __launch_bounds__(kRerankWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
 rerank_certify_kernel(const RerankArgs a) {
     __shared__ float skey[64];
@@ -230,7 +230,7 @@ rerank_certify_kernel(const RerankArgs a) {
     // one list) and the kc smallest land at their ranks — for this kernel (LDS) and the second
     // chance (global).  (The wave threshold select of cand_merge_lane_kernel took ~10 us here:
     // 32 dependent wave-sum steps in one wave while seven waited.)
-    const bool fused = a.l1_G > 0 || a.s_lists > 0;
+    const bool fused = a.l1_G > 0 || (SL && a.s_lists > 0);   // (SL: the instance with s_lists)
     __shared__ float s_mkey[64];
     __shared__ int64_t s_mlab[64];
     __shared__ __attribute__((aligned(16))) uint64_t s_ent[kRerankWaves * 64];
@@ -240,7 +240,7 @@ rerank_certify_kernel(const RerankArgs a) {
     // into s_ent[16 w ..] and the group's floor (the last key of its full lists) into s_gfl[w]
     __shared__ uint64_t s_sel[kRerankWaves][64 + 256];
     __shared__ float s_gfl[kRerankWaves];
-    if (fused && a.s_lists > 0) {
+    if (SL && fused && a.s_lists > 0) {
         // RerankArgs::s_lists: the single-level merge (<= 64 lists of raw_km <= 16 entries: the
         // large batches' per-split lists) by the whole workgroup.  Thread t holds entries t and
         // t + 512; U = the kc-th smallest of the lists' first two entries bounds the answer (kc
@@ -515,7 +515,8 @@ rerank_certify_kernel(const RerankArgs a) {
     // and their max exact key already cuts the rest, so the 16 - k extra rows a 16-row first
     // phase reads are bytes a throughput-bound batch pays for; small batches keep 16 — one round
     // of row loads — since a second phase is a dependent round trip there)
-    const int P1 = a.p1 > 0 ? a.p1 : kRerankWaves * kRerankRows;
+    constexpr int P1max = kRerankWaves * kRerankRows;
+    const int P1 = a.p1 > 0 ? min(a.p1, P1max) : P1max;     // (<= 16: one round of row loads)
     const int m1 = min(m, P1);
     rerank_range(0, m1, std::integral_constant<int, kRerankRows>{});
     __syncthreads();
@@ -656,9 +657,19 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
         return hipErrorInvalidValue;
     if (a.raw_d && (!a.raw_i || !a.chance_list || a.raw_km < a.k || a.raw_lists <= 0))
         return hipErrorInvalidValue;
+    if (a.s_lists > 0 && (a.s_lists > 64 || a.raw_km > 16 || a.raw_lists != a.s_lists || !a.raw_d ||
+                          !a.floor || !a.cd || !a.ci || a.l1_G > 0))
+        return hipErrorInvalidValue;
+    // (the single-level merge has its own instance: its registers stay out of the default one)
 #define IMGREC_RERANK(ITV)                                                                          \
-    hipLaunchKernelGGL((rerank_certify_kernel<ITV>), dim3((unsigned)a.nq), dim3(kRerankWaves * 64), \
-                       0, st, a)
+    do {                                                                                            \
+        if (a.s_lists > 0)                                                                          \
+            hipLaunchKernelGGL((rerank_certify_kernel<ITV, true>), dim3((unsigned)a.nq),             \
+                               dim3(kRerankWaves * 64), 0, st, a);                                  \
+        else                                                                                        \
+            hipLaunchKernelGGL((rerank_certify_kernel<ITV, false>), dim3((unsigned)a.nq),            \
+                               dim3(kRerankWaves * 64), 0, st, a);                                  \
+    } while (0)
     if (a.dp <= 512) IMGREC_RERANK(2);
     else if (a.dp <= 1024) IMGREC_RERANK(4);
     else if (a.dp <= 2048) IMGREC_RERANK(8);

@@ -75,11 +75,19 @@ constexpr int kDeferQ = 3;                // weight waves issue after this quad 
 // that stage before the epilogue instead).  Every CU ends its tiles at the same moment, so a tile
 // end is a 32 MB burst of output stores; waiting for it at the next stage and leaving the lines
 // dirty in the L2 the operand stream runs through cost up to a third of the K = 768 GEMMs
-// (stores skipped: qkv 0.364 -> 0.271 ms).  Measured at batch 512 (profiles/r05/vit_gemm/):
-// qkv 0.357 -> 0.315 ms, proj 0.138 -> 0.110, fc1 + GELU 0.494 -> 0.456, fc2 0.416 -> 0.407.
+// (stores skipped: qkv 0.364 -> 0.271 ms).  Measured at batch 512 (profiles/r05/vit_gemm/), each
+// GEMM alone: qkv 0.357 -> 0.315 ms, proj 0.138 -> 0.110, fc1 + GELU 0.494 -> 0.456, fc2 0.416 ->
+// 0.407; inside the forward the gain mostly does not survive (the next kernel reads an output
+// that was streamed past the MALL): 7,731-7,769 -> 7,783-7,850 images/s with non-temporal stores
+// only for outputs too large for the MALL (policy 2), 7,751-7,811 with all non-temporal
+// (store_policy_forward/).
+// Output store policy (IMGREC_VIT_NT_STORE): 0 plain, 1 non-temporal, 2 non-temporal only when
+// the output exceeds kNtMinBytes (outputs that fit the 256-MB MALL are read back from it by the
+// next kernel; non-temporal lines go to HBM).
 #ifndef IMGREC_VIT_NT_STORE
-#define IMGREC_VIT_NT_STORE 1
+#define IMGREC_VIT_NT_STORE 2
 #endif
+constexpr int64_t kNtMinBytes = 192ll << 20;
 #ifndef IMGREC_VIT_STORE_WAIT
 #define IMGREC_VIT_STORE_WAIT 1
 #endif
@@ -102,7 +110,7 @@ __device__ __forceinline__ float activate(float x) {
     return x;
 }
 
-template <int ACT>
+template <int ACT, bool NT>
 __global__ void __launch_bounds__(512, 2)
 vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww,
                 const float* __restrict__ bias, uint16_t* __restrict__ y, int M, int dw, int N,
@@ -336,12 +344,11 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
 #endif
             {
                 uint4* dst = reinterpret_cast<uint4*>(y + (size_t)tok * N + fcol + ((lq & 1) ? 12 : 0));
-#if IMGREC_VIT_NT_STORE
-                __builtin_nontemporal_store((u32x4){o[0][0], o[0][1], o[1][0], o[1][1]},
-                                            reinterpret_cast<u32x4*>(dst));
-#else
-                *dst = make_uint4(o[0][0], o[0][1], o[1][0], o[1][1]);
-#endif
+                if constexpr (NT)
+                    __builtin_nontemporal_store((u32x4){o[0][0], o[0][1], o[1][0], o[1][1]},
+                                                reinterpret_cast<u32x4*>(dst));
+                else
+                    *dst = make_uint4(o[0][0], o[0][1], o[1][0], o[1][1]);
             }
         }
 #endif
@@ -385,12 +392,19 @@ extern "C" int vit_linear_bf16(const uint16_t* x, const uint16_t* w, const float
     const uint32_t* xw = reinterpret_cast<const uint32_t*>(x);
     const uint32_t* ww = reinterpret_cast<const uint32_t*>(w);
     const hipStream_t st = (hipStream_t)stream;
+    const bool nt = IMGREC_VIT_NT_STORE == 1 || (IMGREC_VIT_NT_STORE == 2 && m * n * 2 > kNtMinBytes);
+#define IMGREC_VIT_LAUNCH(A)                                                                              \
+    do {                                                                                                  \
+        if (nt) hipLaunchKernelGGL((vit_gemm_kernel<A, true>), grid, block, 0, st, xw, ww, bias, y, (int)m, k / 2, n, nsplit, nqb); \
+        else hipLaunchKernelGGL((vit_gemm_kernel<A, false>), grid, block, 0, st, xw, ww, bias, y, (int)m, k / 2, n, nsplit, nqb); \
+    } while (0)
     switch (act) {
-        case VIT_ACT_NONE: hipLaunchKernelGGL((vit_gemm_kernel<VIT_ACT_NONE>), grid, block, 0, st, xw, ww, bias, y, (int)m, k / 2, n, nsplit, nqb); break;
-        case VIT_ACT_GELU_ERF: hipLaunchKernelGGL((vit_gemm_kernel<VIT_ACT_GELU_ERF>), grid, block, 0, st, xw, ww, bias, y, (int)m, k / 2, n, nsplit, nqb); break;
-        case VIT_ACT_GELU_TANH: hipLaunchKernelGGL((vit_gemm_kernel<VIT_ACT_GELU_TANH>), grid, block, 0, st, xw, ww, bias, y, (int)m, k / 2, n, nsplit, nqb); break;
-        case VIT_ACT_QUICK_GELU: hipLaunchKernelGGL((vit_gemm_kernel<VIT_ACT_QUICK_GELU>), grid, block, 0, st, xw, ww, bias, y, (int)m, k / 2, n, nsplit, nqb); break;
+        case VIT_ACT_NONE: IMGREC_VIT_LAUNCH(VIT_ACT_NONE); break;
+        case VIT_ACT_GELU_ERF: IMGREC_VIT_LAUNCH(VIT_ACT_GELU_ERF); break;
+        case VIT_ACT_GELU_TANH: IMGREC_VIT_LAUNCH(VIT_ACT_GELU_TANH); break;
+        case VIT_ACT_QUICK_GELU: IMGREC_VIT_LAUNCH(VIT_ACT_QUICK_GELU); break;
         default: return -1;
     }
+#undef IMGREC_VIT_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
