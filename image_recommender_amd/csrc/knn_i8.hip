@@ -425,7 +425,9 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     Grp A, B;
     int li = wave;
     __shared__ float s_qn[NQ];
-    if (qsrc) {
+    // (the 8-query instance keeps the separate prep: the fused section's registers cost its
+    // VALU-bound main loop ~25 %, profiles/r05/modes_nq/)
+    if (NQ <= 4 && qsrc) {
         // Fused query prep (I8Args::qsrc): wave w derives queries w, w + 4 from the raw rows with
         // i8_query_prep_kernel's arithmetic — the same lane chunks and reductions for the row, its
         // norm and scale, the same quantiser per block — straight into this workgroup's LDS;

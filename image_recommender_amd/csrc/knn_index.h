@@ -102,6 +102,7 @@ struct knn_index {
     int i8_wgpcu = imgrec::kI8WGPCUDefault;
     bool merge_fuse = true;
     bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
+    bool stream_lists = true;   // exact lists of <= 4 queries from one fp32 stream (IMGREC_STREAM_LISTS=0: tiles)
     bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
     bool rerank_p1k = true;     // large batches rerank k rows first (IMGREC_RERANK_P1=0: 16)
     bool i8_fused_prep = true;  // int8 query prep inside the scan (IMGREC_I8_FUSED_PREP=0: own launch)
@@ -217,6 +218,13 @@ bool use_i8(const knn_index* ix, int64_t nq, int k);
 // knn_largek.hip
 int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                   hipStream_t st);
+// Exact per-(query, row split) top-32 lists of <= 4 queries from one fp32 stream of the corpus
+// (csrc/knn_largek.hip largek_stream_kernel): the large-k route's lists and the exact route for
+// small batches; lists at cd / ci + q * sp * 32 + s * 32 (labels with id_offset, -1 = empty).
+bool stream_lists_ok(const knn_index* ix, int64_t nq);
+int stream_splits(const knn_index* ix);
+hipError_t launch_stream_lists(const knn_index* ix, const float* qpad, const float* qnorm, int64_t nq,
+                               int metric, int sp, float* cd, int64_t* ci, hipStream_t st);
 void largek_free(knn_index* ix);
 // merge of nlists sorted per-shard lists for KNN_MAX_K < k (nlists * kin <= 8192; labels < 2^32)
 hipError_t launch_merge_large(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin,

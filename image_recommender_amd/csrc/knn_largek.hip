@@ -118,6 +118,155 @@ __device__ void write_topk(const uint64_t* sel, int k, int metric, int64_t id_of
     }
 }
 
+// Step 1 for small batches (nq <= 4, d <= 4096): the exact fp32 tile kernel computes 32-query tiles, so one
+// query pays for 32 (1M x 1968: 2.9 ms, MFMA-bound on 31 padding queries).  This pass instead
+// streams the fp32 corpus once (HBM-bound: 7.9 GB at 1M x 1968) with VALU dot products: one
+// 4-wave workgroup per row split (8-row groups s, s + nsplit, ... as the int8 scan), a 16-lane
+// group per row, lane j the float4 chunks j, j + 16, ... against the queries' rows in LDS, a DPP
+// row sum, lane j (< NQ) of the group keeping query j's list of 32 (insert_mono: rows arrive in
+// increasing order per lane, so ties keep the smaller row).  The 16 lists of a split fold to its
+// 32 best — the same per-(query, split) lists of exact keys the union certifies (a row a lane
+// list dropped has a key >= that list's 32nd >= the folded list's 32nd).  Keys are the exact
+// kernel's form, (|q|^2 + |x|^2) - 2 q.x clamped at 0 or -q.x, the dot summed in this kernel's
+// own fp32 order.
+template <int K>
+__device__ __forceinline__ void lk_insert(float (&kd)[K], int (&ki)[K], float d, int id) {
+    bool c[K];
+#pragma unroll
+    for (int p = 0; p < K; ++p) c[p] = d < kd[p];
+#pragma unroll
+    for (int p = K - 1; p > 0; --p) {
+        kd[p] = __builtin_amdgcn_fmed3f(kd[p - 1], d, kd[p]);
+        const int nx = c[p] ? id : ki[p];
+        ki[p] = c[p - 1] ? ki[p - 1] : nx;
+    }
+    kd[0] = c[0] ? d : kd[0];
+    ki[0] = c[0] ? id : ki[0];
+}
+
+__device__ __forceinline__ float lk_row16_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false));
+    return v;
+}
+
+constexpr int kLKSW = 4;            // waves of the streaming pass
+constexpr int kLKSDp = 4096;        // widest padded row of the streaming pass (query rows in LDS)
+
+template <int NQ>
+__global__ void __launch_bounds__(kLKSW * 64) __attribute__((amdgpu_waves_per_eu(2)))
+largek_stream_kernel(const float* __restrict__ xb, const float* __restrict__ xn, int nrows, int dp,
+                     const float* __restrict__ qpad, const float* __restrict__ qnorm, int nq,
+                     int nsplit, int metric, int64_t id_offset, float* __restrict__ cand_d,
+                     int64_t* __restrict__ cand_i, int ncand) {
+    constexpr int KM = KNN_MAX_K;
+    __shared__ __attribute__((aligned(16))) float sq[NQ * kLKSDp];
+    __shared__ float fd[NQ][16][KM];
+    __shared__ int fi[NQ][16][KM];
+    const int split = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int j = lane & 15, g = lane >> 4;
+    const int n4 = dp / 4;
+    for (int i = tid; i < NQ * n4; i += kLKSW * 64) {
+        const int qi = i / n4;
+        reinterpret_cast<float4*>(sq)[i] = qi < nq ? reinterpret_cast<const float4*>(qpad)[(int64_t)qi * n4 + (i - qi * n4)]
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float qn[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) qn[q] = (metric == 1 && q < nq) ? qnorm[q] : 0.f;
+    __syncthreads();
+    float kd[KM];
+    int ki[KM];
+#pragma unroll
+    for (int p = 0; p < KM; ++p) { kd[p] = INFINITY; ki[p] = -1; }
+    const bool owner = j < NQ && j < nq;
+    const int ngroups = (nrows + 7) / 8;
+    // a wave step: the 4 rows 4 h + g of an 8-row group (two steps per group)
+    const int cnt = 2 * (split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0);
+    const float4* sq4 = reinterpret_cast<const float4*>(sq);
+    for (int li = wave; li < cnt; li += kLKSW) {
+        const int m = split + (li >> 1) * nsplit;
+        const int row = m * 8 + 4 * (li & 1) + g;
+        const int rc = min(row, nrows - 1);
+        const float4* x4 = reinterpret_cast<const float4*>(xb + (int64_t)rc * dp);
+        float acc[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+        // 8 chunks in flight per lane (128 B), then their products
+        for (int c0 = j; c0 < n4; c0 += 16 * 8) {
+            float4 xv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int c = c0 + 16 * u;
+                typedef float f32x4v __attribute__((ext_vector_type(4)));
+                if (c < n4) {
+                    const f32x4v w = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(x4 + c));
+                    xv[u] = make_float4(w.x, w.y, w.z, w.w);
+                } else {
+                    xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int c = min(c0 + 16 * u, n4 - 1);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    const float4 qv = sq4[q * n4 + c];
+                    acc[q] = fmaf(xv[u].x, qv.x, acc[q]);
+                    acc[q] = fmaf(xv[u].y, qv.y, acc[q]);
+                    acc[q] = fmaf(xv[u].z, qv.z, acc[q]);
+                    acc[q] = fmaf(xv[u].w, qv.w, acc[q]);
+                }
+            }
+        }
+        const float xnr = metric == 1 ? xn[rc] : 0.f;
+        float kv = INFINITY;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float dot = lk_row16_sum(acc[q]);
+            const float key = metric == 1 ? fmaxf((qn[q] + xnr) - 2.f * dot, 0.f) : -dot;
+            kv = j == q ? key : kv;
+        }
+        kv = (owner && row < nrows && kv < kd[KM - 1]) ? kv : INFINITY;
+        if (__any(kv != INFINITY)) lk_insert<KM>(kd, ki, kv, row);
+    }
+    // fold the split's 16 lists of each query (4 waves x 4 row groups) into its 32 best
+    if (owner) {
+#pragma unroll
+        for (int p = 0; p < KM; ++p) {
+            fd[j][wave * 4 + g][p] = kd[p];
+            fi[j][wave * 4 + g][p] = ki[p];
+        }
+    }
+    __syncthreads();
+    const int fq = wave * 4 + (lane >> 4), fl = lane & 15;
+    if (fq >= NQ || fq >= nq) return;                    // (whole 16-lane groups leave together)
+    int pos = 0;
+    for (int p = 0; p < KM; ++p) {
+        float hk = pos < KM ? fd[fq][fl][pos] : INFINITY;
+        int hl = pos < KM ? fi[fq][fl][pos] : -1;
+        if (hl < 0) hk = INFINITY;
+        float bk = hk;
+        int bl = hl < 0 ? 0x7fffffff : hl;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            const float ok = __shfl_xor(bk, o, 16);
+            const int ol = __shfl_xor(bl, o, 16);
+            if (ok < bk || (ok == bk && ol < bl)) { bk = ok; bl = ol; }
+        }
+        const bool won = hk == bk && (hl < 0 ? 0x7fffffff : hl) == bl && bk != INFINITY;
+        if (won) ++pos;
+        if (fl == 0) {
+            const int64_t o = (int64_t)fq * ncand + (int64_t)split * KM + p;
+            cand_d[o] = bk;
+            cand_i[o] = bk == INFINITY ? (int64_t)-1 : (int64_t)bl + id_offset;
+        }
+    }
+}
+
 // Step 2 (module doc): a workgroup per query of the block.  cd / ci: the tile kernel's lists
 // (nlists of km ascending keys per query, stride ncand; labels with id_offset, -1 = empty).
 // Certified queries are written to D / I; the others go to fail_list (with their union's k-th
@@ -287,6 +436,32 @@ hipError_t launch_merge_large(const float* cD, const int64_t* cI, int nlists, in
     return hipGetLastError();
 }
 
+// (rows narrower than 128 floats leave most of a row's 16 lanes idle: one query on 1M x 48
+// colour rows streams in 0.221 ms against the tile kernel's 0.207 — profiles/r05/stream/)
+bool stream_lists_ok(const knn_index* ix, int64_t nq) {
+    return ix->stream_lists && nq >= 1 && nq <= 4 && ix->dp >= 128 && ix->dp <= kLKSDp && ix->dp % 4 == 0;
+}
+
+int stream_splits(const knn_index* ix) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)ix->cus * 2, (ix->ntotal + 7) / 8));
+}
+
+// The streaming list pass (largek_stream_kernel): nq <= 4 padded queries, sp row splits, the
+// lists at cd / ci + q * sp * 32 + s * 32.
+hipError_t launch_stream_lists(const knn_index* ix, const float* qpad, const float* qnorm, int64_t nq,
+                               int metric, int sp, float* cd, int64_t* ci, hipStream_t st) {
+    if (nq < 1 || nq > 4 || ix->dp % 4 != 0 || ix->dp > kLKSDp || sp < 1) return hipErrorInvalidValue;
+#define IMGREC_LKS(NQV)                                                                            \
+    hipLaunchKernelGGL((largek_stream_kernel<NQV>), dim3((unsigned)sp), dim3(kLKSW * 64), 0, st, ix->xb, \
+                       ix->xn, (int)ix->ntotal, ix->dp, qpad, qnorm, (int)nq, sp, metric,          \
+                       ix->id_offset, cd, ci, sp * KNN_MAX_K)
+    if (nq == 1) IMGREC_LKS(1);
+    else if (nq == 2) IMGREC_LKS(2);
+    else IMGREC_LKS(4);
+#undef IMGREC_LKS
+    return hipGetLastError();
+}
+
 void largek_free(knn_index* ix) {
     for (void* p : {(void*)ix->lk_run, (void*)ix->lk_fail})
         if (p) (void)hipFree(p);
@@ -314,26 +489,38 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
         const int64_t qc = std::min<int64_t>(kQueryChunk, nq - q0);
         const Plan p = make_plan(ix->ntotal, qc, KNN_MAX_K, ix->cus);     // KM = 32 lists
+        // <= 4 queries whose rows fit the streaming pass's LDS: lists from one fp32 stream of the
+        // corpus instead of 32-query tiles (IMGREC_STREAM_LISTS=0 at index creation: tiles)
+        const bool stream = stream_lists_ok(ix, qc);
+        const int sp = stream_splits(ix);
+        const size_t ncap = std::max<size_t>((size_t)p.ncand, (size_t)sp * KNN_MAX_K);
         if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)p.nq_pad * ix->dp)) != KNN_OK) return rc;
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)p.nq_pad)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)qc * p.ncand)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)qc * p.ncand)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)qc * ncap)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)qc * ncap)) != KNN_OK) return rc;
         if ((rc = grow(&ix->lk_fail, &ix->lk_fail_cap, (size_t)qc + 1)) != KNN_OK) return rc;
         KNN_HIP(launch_rows_ingest(q + q0 * ix->d, qc, ix->d, ix->dp, p.nq_pad,
                                    ix->metric == KNN_METRIC_COSINE ? 1 : 0, ix->qpad, ix->qnorm, st));
-        TileArgs a{};
-        a.wr = p.wr; a.wq = p.wq; a.km = p.km;
-        a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
-        a.qp = ix->qpad; a.qnorm = ix->qnorm; a.nq = (int)qc; a.metric = kmetric;
-        a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
-        a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.mode = kModeF32;
-        KNN_HIP(launch_tile_topk(a, st));
+        int nlists = p.ncand / p.km, ncand = p.ncand;
+        if (stream) {
+            KNN_HIP(launch_stream_lists(ix, ix->qpad, ix->qnorm, qc, kmetric, sp, ix->cand_d, ix->cand_i, st));
+            nlists = sp;
+            ncand = sp * KNN_MAX_K;
+        } else {
+            TileArgs a{};
+            a.wr = p.wr; a.wq = p.wq; a.km = p.km;
+            a.xb = ix->xb; a.xnorm = ix->xn; a.nrows = (int)ix->ntotal; a.dp = ix->dp;
+            a.qp = ix->qpad; a.qnorm = ix->qnorm; a.nq = (int)qc; a.metric = kmetric;
+            a.ntiles = p.ntiles; a.nsplit = p.nsplit; a.nqb = p.nqb; a.id_offset = ix->id_offset;
+            a.cand_d = ix->cand_d; a.cand_i = ix->cand_i; a.ncand = p.ncand; a.mode = kModeF32;
+            KNN_HIP(launch_tile_topk(a, st));
+        }
         float* Db = D + q0 * k;
         int64_t* Ib = I + q0 * k;
         int* cnt = ix->lk_fail + qc;
         KNN_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
         hipLaunchKernelGGL(largek_union_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st, ix->cand_d,
-                           ix->cand_i, p.ncand / p.km, p.km, p.ncand, k, ix->ntotal, kmetric,
+                           ix->cand_i, nlists, KNN_MAX_K, ncand, k, ix->ntotal, kmetric,
                            ix->id_offset, Db, Ib, ix->lk_fail, cnt);
         KNN_HIP(hipGetLastError());
         // the certificate's leftovers: the host reads their count (this path's only wait)

@@ -42,8 +42,24 @@ int timed_begin(knn_index* ix, hipStream_t st, hipEvent_t* e1) {
 int exact_chunk(knn_index* ix, const float* qpad, const float* qnorm, int64_t nq, int k, float* D,
                 int64_t* I, hipStream_t st, bool timed) {
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
-    const Plan p = make_plan(ix->ntotal, nq, k, ix->cus);
     int rc;
+    if (stream_lists_ok(ix, nq)) {
+        // <= 4 queries: the corpus streamed once (HBM-bound) into exact lists of 32 per row
+        // split, merged — instead of 32-query fp32 MFMA tiles that compute 28-31 padding queries
+        // (d = 48 colour-only or d = 1968 exact mode, one query on 1M rows; profiles/r05/stream/)
+        const int sp = stream_splits(ix);
+        const size_t nc = (size_t)sp * KNN_MAX_K;
+        if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * nc)) != KNN_OK) return rc;
+        if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * nc)) != KNN_OK) return rc;
+        hipEvent_t e1 = nullptr;
+        if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
+        KNN_HIP(launch_stream_lists(ix, qpad, qnorm, nq, kmetric, sp, ix->cand_d, ix->cand_i, st));
+        if (e1) KNN_HIP(hipEventRecord(e1, st));
+        KNN_HIP(launch_merge(ix->cand_d, ix->cand_i, nq, sp, KNN_MAX_K, (int64_t)nc, KNN_MAX_K, k,
+                             kmetric, 0, D, I, st));
+        return KNN_OK;
+    }
+    const Plan p = make_plan(ix->ntotal, nq, k, ix->cus);
     if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
     TileArgs a{};
@@ -425,13 +441,20 @@ bool use_b16(const knn_index* ix, int64_t nq, int k) {
 // enough (<= 64 MB, ~10 us of streaming) for the fixed costs to decide.
 constexpr int kI8AutoQ = 8;
 constexpr int kI8MinBlocks = 8;
+// 5-8 queries run the scan's 8-query instance, VALU-bound: its time steps with the blocks per
+// lane (NBI = ceil(blocks / 16)), the bf16 pass's grows with d.  One box, 1M rows
+// (profiles/r05/modes_nq/, small_d/): 8 queries int8 / bf16 0.355 / 0.326 ms at 12 blocks,
+// 0.339 / 0.397 at 16, 0.530 / 0.496 at 20, 0.585 / 0.679 at 31 — the int8 route at 14-16 blocks
+// and from 23
+bool i8_wins_8q(int nblk) { return (nblk >= 14 && nblk <= 16) || nblk >= 23; }
 constexpr int64_t kI8SmallCopyBytes = 64ll << 20;
 bool use_i8(const knn_index* ix, int64_t nq, int k) {
     if (ix->nblk8 <= 0 || k > KNN_MAX_K || nq > kI8MaxQ) return false;
     if (ix->mode == KNN_SEARCH_I8) return true;
     if (ix->mode != KNN_SEARCH_AUTO || nq > kI8AutoQ) return false;
     const int64_t i8_row = i8_row_bytes(ix->nblk8) + 4 * ix->nblk8;
-    return !ix->b16_ok || nq <= 2 || ix->nblk8 >= kI8MinBlocks || ix->ntotal * i8_row <= kI8SmallCopyBytes;
+    const bool wide_enough = nq <= 2 ? true : nq <= 4 ? ix->nblk8 >= kI8MinBlocks : i8_wins_8q(ix->nblk8);
+    return !ix->b16_ok || wide_enough || ix->ntotal * i8_row <= kI8SmallCopyBytes;
 }
 
 bool use_split(const knn_index* ix, int64_t nq, int k) {
@@ -477,7 +500,7 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         // the same rows and norms + the two-level int8 codes (one short pass instead of
         // rows_ingest's latency-bound row loop and a second launch)
         // (the int8 path's prep runs inside its scan unless IMGREC_I8_FUSED_PREP=0: nq_pad = cn)
-        const bool i8_fused = i8 && ix->i8_fused_prep && nq_pad == cn;
+        const bool i8_fused = i8 && ix->i8_fused_prep && nq_pad == cn && cn <= 4;
         if (i8) {
             if ((rc = grow(&ix->q8r, &ix->q8r_cap, (size_t)cn)) != KNN_OK) return rc;
         }

@@ -44,8 +44,10 @@ def test_large_k_one_million_rows(faiss, nq, k):
     check_knn(D[sel], I[sel], xb, xq[sel], k, "l2", min_exact_frac=0.5)
 
 
-def test_large_k_fallback_on_a_crowded_list(faiss):
-    """64 exact duplicates of the query on the rows ONE fused-kernel list owns: the exact kernel's
+def test_large_k_fallback_on_a_crowded_list(faiss, monkeypatch):
+    """(The tile-kernel lists: IMGREC_STREAM_LISTS=0; one query would otherwise take the
+    streaming pass, whose lists are per row split — next test.)
+    64 exact duplicates of the query on the rows ONE fused-kernel list owns: the exact kernel's
     row split 0 takes tile 0 (split s takes tiles s, s + nsplit, ...), its wave-row 0 holds the
     tile's rows 0-127 and lane half 0 of the 32 x 32 accumulator the rows 0-3 mod 8 of them
     (csrc/knn_kernels.hip tile_topk_item).  That list keeps 32 of the duplicates, its 32nd key (0)
@@ -57,7 +59,9 @@ def test_large_k_fallback_on_a_crowded_list(faiss):
     rows = np.array([r for r in range(128) if r % 8 < 4])
     assert len(rows) == 64
     xb[rows] = q[0]
-    idx = faiss.IndexFlatL2(d)
+    monkeypatch.setenv("IMGREC_STREAM_LISTS", "0")
+    idx = faiss.IndexFlatL2(d)                              # (knobs are read at creation)
+    monkeypatch.delenv("IMGREC_STREAM_LISTS")
     idx.add(xb)
     D, I = idx.search(q, k)
     assert _fallbacks(idx) == 1
@@ -81,3 +85,52 @@ def test_large_k_fallback_when_lists_hold_fewer_than_k(faiss, metric):
     D, I = idx.search(xq, 1000)
     assert _fallbacks(idx) == 5
     check_knn(D, I, xb, xq, 1000, metric, min_exact_frac=0.0)
+
+
+def _stream_splits():
+    import torch
+    return 2 * torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def test_large_k_stream_lists_crowded_split(faiss):
+    """The streaming pass (<= 4 queries, csrc/knn_largek.hip largek_stream_kernel) keeps one list of
+    32 per row split, split s owning the 8-row groups s, s + S, ... (S = 2 x CUs).  40 duplicates
+    of the query on split 0's rows fill its list with key 0: that floor sits below the union's
+    100th key, the certificate fails and the exact scan answers — all 40 duplicates first, in
+    label order."""
+    n, d, k = 300_000, 160, 100                          # (the pass takes rows of >= 128 floats)
+    S = _stream_splits()
+    xb = mixture(n, d, centres=200, seed=15)
+    q = mixture(1, d, centres=200, seed=16)
+    rows = np.array([8 * S * i + t for i in range(5) for t in range(8)])
+    assert rows.max() < n and len(rows) == 40
+    xb[rows] = q[0]
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    D, I = idx.search(q, k)
+    assert _fallbacks(idx) == 1
+    assert (I[0, :40] == rows).all() and (D[0, :40] <= 1e-4 * float((q[0] ** 2).sum())).all()
+    check_knn(D, I, xb, q, k, "l2", min_exact_frac=0.0)
+
+
+@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
+@pytest.mark.parametrize("nq", [1, 2, 4])
+def test_large_k_stream_pass_against_tiles_and_oracle(faiss, monkeypatch, metric, nq):
+    """1-4 queries on the streaming pass and on the tile lists (IMGREC_STREAM_LISTS=0): both
+    certified (no fallback), the same labels wherever the float64 oracle separates the ranks, and
+    each within the stated fp32 tolerance of float64 (tests/knn_check.py)."""
+    n, d, k = 200_000, 200, 128
+    xb = mixture(n, d, centres=300, seed=nq + 30)
+    xq = mixture(nq, d, centres=300, seed=nq + 31)
+    mk = {"l2": faiss.IndexFlatL2, "ip": faiss.IndexFlatIP,
+          "cosine": lambda dd: faiss.IndexFlat(dd, faiss.METRIC_COSINE)}[metric]
+    out = {}
+    for name, env in (("stream", None), ("tiles", "0")):
+        if env is not None:
+            monkeypatch.setenv("IMGREC_STREAM_LISTS", env)
+        idx = mk(d)
+        monkeypatch.delenv("IMGREC_STREAM_LISTS", raising=False)
+        idx.add(xb)
+        out[name] = idx.search(xq, k)
+        assert _fallbacks(idx) == 0, name
+        check_knn(out[name][0], out[name][1], xb, xq, k, metric, min_exact_frac=0.5)

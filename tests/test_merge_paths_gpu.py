@@ -60,7 +60,8 @@ VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "level2only": {"IMGREC_MERGE_
 
 @pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257, 1024])
 def test_routes_return_identical_bits(corpus, monkeypatch, nq):
-    """nq 1-8: the int8 path (split counts 1-5 per CU, fused or separate level 2); nq = 16: the
+    """nq 1-2: the int8 path (split counts 1-5 per CU, fused or separate level 2); 5 and 8 at
+    d = 768 the bf16 small-batch tile (the int8 route's 8-query instance loses at 12 blocks); 16: the
     bf16 path's small-batch tile with the fused or separate level 2; 256 / 257: the last batch
     that fuses (one rerank workgroup per CU) and the first that does not.  The float64 oracle
     checks the default route on up to 16 of the queries."""
