@@ -282,6 +282,7 @@ int create_single(int d, int metric, int device, knn_index** out) {
     if (const char* e = test_knob("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
     if (const char* e = test_knob("IMGREC_I8_FUSED_PREP")) ix->i8_fused_prep = *e != '0';
     if (const char* e = test_knob("IMGREC_RERANK_P1")) ix->rerank_p1k = *e != '0';
+    if (const char* e = test_knob("IMGREC_RERANK_NW4")) ix->rerank_nw4 = *e != '0';
     if (const char* e = test_knob("IMGREC_MERGE_SINGLE")) ix->merge_single = *e != '0';
     if (const char* e = test_knob("IMGREC_STREAM_LISTS")) ix->stream_lists = *e != '0';
     if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess ||

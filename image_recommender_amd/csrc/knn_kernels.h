@@ -83,6 +83,7 @@ struct RerankArgs {
     // lists of raw_km <= 16 entries are selected by the whole workgroup (large batches' single
     // level; no merge launch)
     int s_lists = 0;
+    int nw = 0;                 // rerank workgroup waves: 0 = kRerankWaves (8), 4 = large batches
     int p1 = 0;                 // first-phase rerank size (0 = kRerankWaves x kRerankRows = 16);
                                 // large batches use k: their rerank is bound by row bytes
     int chance_skip = 0;        // queue a query whose band certainly-ish exceeds K' straight to the

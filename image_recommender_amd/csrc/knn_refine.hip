@@ -195,8 +195,11 @@ query_prep_b16_kernel(const float* __restrict__ src, int64_t n, int d, int dp, i
 // query with the rows (any dp).
 // A query whose certificate fails goes to the second-chance queue (a.raw_d set: stats[3] counts
 // it) or straight to the exact re-run list (stats[0]).
-template <int IT, bool SL>
-__global__ void __launch_bounds__(kRerankWaves * 64) __attribute__((amdgpu_waves_per_eu(4)))
+// NW waves per workgroup: 8, or 4 for large batches (RerankArgs::nw; no fused merge there): at
+// the register budget of four waves per SIMD a CU then holds four workgroups instead of two, so a
+// 1024-query batch reranks in one round of resident workgroups instead of two.
+template <int IT, bool SL, int NW>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4)))
 rerank_certify_kernel(const RerankArgs a) {
     __shared__ float skey[64];
     __shared__ int64_t slab[64];
@@ -230,7 +233,7 @@ rerank_certify_kernel(const RerankArgs a) {
     // one list) and the kc smallest land at their ranks — for this kernel (LDS) and the second
     // chance (global).  (The wave threshold select of cand_merge_lane_kernel took ~10 us here:
     // 32 dependent wave-sum steps in one wave while seven waited.)
-    const bool fused = a.l1_G > 0 || (SL && a.s_lists > 0);   // (SL: the instance with s_lists)
+    const bool fused = NW == kRerankWaves && (a.l1_G > 0 || (SL && a.s_lists > 0));   // (SL: the instance with s_lists)
     __shared__ float s_mkey[64];
     __shared__ int64_t s_mlab[64];
     __shared__ __attribute__((aligned(16))) uint64_t s_ent[kRerankWaves * 64];
@@ -488,19 +491,19 @@ rerank_certify_kernel(const RerankArgs a) {
     };
     // the lane's own candidate's |x|^2, loaded up front (not after each round's dot products)
     const float xn_own = valid ? a.xn[lab - id_offset] : 0.f;
-    // candidates [c_begin, c_end), kRerankWaves * R rows in flight per round
+    // candidates [c_begin, c_end), NW * R rows in flight per round
     auto rerank_range = [&](int c_begin, int c_end, auto r_tag) {
         constexpr int R = decltype(r_tag)::value;
-        for (int c0 = c_begin + wave; c0 < c_end; c0 += kRerankWaves * R) {
+        for (int c0 = c_begin + wave; c0 < c_end; c0 += NW * R) {
             const float4* r4[R];
             float acc[R];
 #pragma unroll
             for (int v = 0; v < R; ++v)
-                r4[v] = row_of(min(c0 + kRerankWaves * v, c_end - 1));   // clamped: loads unconditional
+                r4[v] = row_of(min(c0 + NW * v, c_end - 1));   // clamped: loads unconditional
             rerank_dots<IT, R>(q4, qr, n4, lane, r4, acc);
 #pragma unroll
             for (int v = 0; v < R; ++v) {
-                const int c = c0 + kRerankWaves * v;
+                const int c = c0 + NW * v;
                 if (lane == c && c < c_end) skey[c] = rerank_key(acc[v], B.qn, xn_own, metric);
             }
         }
@@ -515,8 +518,8 @@ rerank_certify_kernel(const RerankArgs a) {
     // and their max exact key already cuts the rest, so the 16 - k extra rows a 16-row first
     // phase reads are bytes a throughput-bound batch pays for; small batches keep 16 — one round
     // of row loads — since a second phase is a dependent round trip there)
-    constexpr int P1max = kRerankWaves * kRerankRows;
-    const int P1 = a.p1 > 0 ? min(a.p1, P1max) : P1max;     // (<= 16: one round of row loads)
+    constexpr int P1max = kRerankWaves * kRerankRows;   // (16: one round of loads at NW = 8)
+    const int P1 = a.p1 > 0 ? min(a.p1, P1max) : P1max;
     const int m1 = min(m, P1);
     rerank_range(0, m1, std::integral_constant<int, kRerankRows>{});
     __syncthreads();
@@ -660,14 +663,19 @@ hipError_t launch_rerank_certify(const RerankArgs& a, hipStream_t st) {
     if (a.s_lists > 0 && (a.s_lists > 64 || a.raw_km > 16 || a.raw_lists != a.s_lists || !a.raw_d ||
                           !a.floor || !a.cd || !a.ci || a.l1_G > 0))
         return hipErrorInvalidValue;
+    if (a.nw != 0 && (a.nw != 4 || a.s_lists > 0 || a.l1_G > 0 || a.chance_skip))
+        return hipErrorInvalidValue;
     // (the single-level merge has its own instance: its registers stay out of the default one)
 #define IMGREC_RERANK(ITV)                                                                          \
     do {                                                                                            \
-        if (a.s_lists > 0)                                                                          \
-            hipLaunchKernelGGL((rerank_certify_kernel<ITV, true>), dim3((unsigned)a.nq),             \
+        if (a.nw == 4)                                                                              \
+            hipLaunchKernelGGL((rerank_certify_kernel<ITV, false, 4>), dim3((unsigned)a.nq),         \
+                               dim3(4 * 64), 0, st, a);                                             \
+        else if (a.s_lists > 0)                                                                     \
+            hipLaunchKernelGGL((rerank_certify_kernel<ITV, true, kRerankWaves>), dim3((unsigned)a.nq), \
                                dim3(kRerankWaves * 64), 0, st, a);                                  \
         else                                                                                        \
-            hipLaunchKernelGGL((rerank_certify_kernel<ITV, false>), dim3((unsigned)a.nq),            \
+            hipLaunchKernelGGL((rerank_certify_kernel<ITV, false, kRerankWaves>), dim3((unsigned)a.nq), \
                                dim3(kRerankWaves * 64), 0, st, a);                                  \
     } while (0)
     if (a.dp <= 512) IMGREC_RERANK(2);

@@ -70,11 +70,6 @@ add_ln_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta, const f
 // so every access is one 16-B (fp32) or 8-B (bf16) vector per lane — 1 KiB / 512 B per wave
 // instruction instead of the 256 B / 128 B of the lane-strided form (round 3: 221 us per call
 // at 100,864 x 768 rows = 4.2 TB/s for that form, profiles/r03/).
-#ifndef IMGREC_VIT_LN_XNT
-#define IMGREC_VIT_LN_XNT 0
-#endif
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-
 template <int CH>
 __global__ void __launch_bounds__(256)
 add_ln_vec_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta, const float* __restrict__ g,
@@ -99,13 +94,9 @@ add_ln_vec_kernel(float* __restrict__ x, const uint16_t* __restrict__ delta, con
             v[i].y += __uint_as_float(dl[i].x & 0xffff0000u);
             v[i].z += __uint_as_float(dl[i].y << 16);
             v[i].w += __uint_as_float(dl[i].y & 0xffff0000u);
-#if IMGREC_VIT_LN_XNT
-            // (the residual is next read two GEMMs and an attention later: past the MALL anyway)
-            __builtin_nontemporal_store((f32x4v){v[i].x, v[i].y, v[i].z, v[i].w},
-                                        reinterpret_cast<f32x4v*>(xr + lane + 64 * i));
-#else
+            // (a non-temporal form of this store measured the same in the forward:
+            // profiles/r05/vit_gemm/store_policy_forward/ab_vit_ln_residual_nt.jsonl)
             xr[lane + 64 * i] = v[i];
-#endif
         }
         s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     }
