@@ -104,7 +104,7 @@ struct knn_index {
     bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
     bool stream_lists = true;   // exact lists of <= 4 queries from one fp32 stream (IMGREC_STREAM_LISTS=0: tiles)
     bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
-    bool rerank_nw4 = true;     // large batches rerank on 4-wave workgroups (IMGREC_RERANK_NW4=0: 8)
+    bool rerank_nw4 = false;    // IMGREC_RERANK_NW4=1: large batches rerank on 4-wave workgroups
     bool rerank_p1k = true;     // large batches rerank k rows first (IMGREC_RERANK_P1=0: 16)
     bool i8_fused_prep = true;  // int8 query prep inside the scan (IMGREC_I8_FUSED_PREP=0: own launch)
     bool merge_fuse1 = true;    // IMGREC_MERGE_FUSE=1: only level 2 in the rerank (0: neither)

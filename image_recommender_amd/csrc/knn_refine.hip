@@ -195,9 +195,9 @@ query_prep_b16_kernel(const float* __restrict__ src, int64_t n, int d, int dp, i
 // query with the rows (any dp).
 // A query whose certificate fails goes to the second-chance queue (a.raw_d set: stats[3] counts
 // it) or straight to the exact re-run list (stats[0]).
-// NW waves per workgroup: 8, or 4 for large batches (RerankArgs::nw; no fused merge there): at
-// the register budget of four waves per SIMD a CU then holds four workgroups instead of two, so a
-// 1024-query batch reranks in one round of resident workgroups instead of two.
+// NW waves per workgroup: 8, or 4 (RerankArgs::nw, opt-in for large batches; no fused merge
+// there): at the register budget of four waves per SIMD a CU then holds four workgroups instead
+// of two — measured no faster (profiles/r05/rerank_nw4_ab/).
 template <int IT, bool SL, int NW>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4)))
 rerank_certify_kernel(const RerankArgs a) {

@@ -162,8 +162,9 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     // first rerank phase of k rows for batches past one rerank workgroup per CU
     // (IMGREC_RERANK_P1: 0 keeps 16 everywhere, for A/B)
     r.p1 = ix->rerank_p1k && nq > ix->cus ? k : 0;
-    // 4-wave rerank workgroups past one per CU (four resident per CU, one round for 1024 queries;
-    // IMGREC_RERANK_NW4=0: 8 waves)
+    // 4-wave rerank workgroups past one per CU (four resident per CU, one round for 1024 queries):
+    // opt-in (IMGREC_RERANK_NW4=1) — measured 3-4 us slower per 125k-row step than 8 waves, the
+    // rerank is not residency-bound (profiles/r05/rerank_nw4_ab/)
     r.nw = ix->rerank_nw4 && nq > ix->cus && r.l1_G == 0 && r.s_lists == 0 && !r.chance_skip ? 4 : 0;
     KNN_HIP(launch_rerank_certify(r, st));
     TailArgs t{};
