@@ -78,16 +78,19 @@ constexpr int kDeferQ = 3;                // weight waves issue after this quad 
 // (stores skipped: qkv 0.364 -> 0.271 ms).  Measured at batch 512 (profiles/r05/vit_gemm/), each
 // GEMM alone: qkv 0.357 -> 0.315 ms, proj 0.138 -> 0.110, fc1 + GELU 0.494 -> 0.456, fc2 0.416 ->
 // 0.407; inside the forward the gain mostly does not survive (the next kernel reads an output
-// that was streamed past the MALL): 7,731-7,769 -> 7,783-7,850 images/s with non-temporal stores
-// only for outputs too large for the MALL (policy 2), 7,751-7,811 with all non-temporal
+// that was streamed past the MALL; per kernel in the forward the qkv GEMM even got slower,
+// forward_kernels/): batch 512 on one box 7,620 images/s (round-4 stores) -> 7,640 (non-temporal
+// from 192 MB: qkv and fc1) -> 7,690 (from 512 MB: fc1's 620 MB output only, the default)
 // (store_policy_forward/).
 // Output store policy (IMGREC_VIT_NT_STORE): 0 plain, 1 non-temporal, 2 non-temporal only when
-// the output exceeds kNtMinBytes (outputs that fit the 256-MB MALL are read back from it by the
-// next kernel; non-temporal lines go to HBM).
+// the output exceeds kNtMinBytes (IMGREC_VIT_NT_MIN_MB).
 #ifndef IMGREC_VIT_NT_STORE
 #define IMGREC_VIT_NT_STORE 2
 #endif
-constexpr int64_t kNtMinBytes = 192ll << 20;
+#ifndef IMGREC_VIT_NT_MIN_MB
+#define IMGREC_VIT_NT_MIN_MB 512
+#endif
+constexpr int64_t kNtMinBytes = (int64_t)IMGREC_VIT_NT_MIN_MB << 20;
 #ifndef IMGREC_VIT_STORE_WAIT
 #define IMGREC_VIT_STORE_WAIT 1
 #endif
