@@ -46,6 +46,17 @@ constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA pi
 constexpr bool kNtCodes = IMGREC_I8_NT != 0;   // non-temporal code loads in the scan
 
 
+#ifdef IMGREC_I8_STAMPS
+// diagnostic build only (tools/i8_stamps.py): s_memrealtime (100 MHz, one clock for the chip) per
+// scan workgroup (< 1024): 0 entry, 1 query side in LDS, 2 first group processed (wave 0),
+// 3-6 waves 0-3 leave the row loop, 7 lists written
+__device__ unsigned long long g_i8_stamps[1024 * 8];
+#define I8_STAMP(slot) do { if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) \
+    g_i8_stamps[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define I8_STAMP(slot) do {} while (0)
+#endif
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -292,6 +303,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int j = lane & 15, g = lane >> 4;
     const int64_t rowb = i8_row_bytes(nblk);
+    if (wave == 0) I8_STAMP(0);
     float qn[NQ];
     float kd[KM];
     int ki[KM];
@@ -545,10 +557,13 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
 
     // (the first group's loads issued before the query prep instead measured the same:
     // profiles/r05/nq1/preload/)
+    if (wave == 0) I8_STAMP(1);
     if (li < cnt) load(li, A);
+    bool first_done = false;
     while (li < cnt) {
         if (li + kWaves < cnt) load(li + kWaves, B);
         process(A);
+        if (wave == 0 && !first_done) { I8_STAMP(2); first_done = true; }
         li += kWaves;
         if (li >= cnt) break;
         if (li + kWaves < cnt) load(li + kWaves, A);
@@ -556,6 +571,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         li += kWaves;
     }
 
+    I8_STAMP(3 + wave);
     // fold the split's 16 lists of each query (4 waves x 4 row groups) into one list of KM
     __syncthreads();                                     // (every wave is done with the codes)
     if (owner) {
@@ -591,6 +607,12 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
             cand_i[o] = bk == INFINITY ? (int64_t)-1 : (int64_t)bl + id_offset;
         }
     }
+#ifdef IMGREC_I8_STAMPS
+    if (fq == 0 && fl == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        g_i8_stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 }  // namespace
@@ -662,3 +684,13 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
 }
 
 }  // namespace imgrec
+
+#ifdef IMGREC_I8_STAMPS
+extern "C" int knn_i8_stamps_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(imgrec::g_i8_stamps), sizeof(imgrec::g_i8_stamps));
+}
+extern "C" int knn_i8_stamps_clear() {
+    static unsigned long long zero[1024 * 8];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(imgrec::g_i8_stamps), zero, sizeof(zero));
+}
+#endif
