@@ -33,6 +33,7 @@
 #include <math.h>
 
 #include "knn_kernels.h"
+#include "wave_ops.h"
 
 namespace imgrec {
 namespace {
@@ -44,6 +45,9 @@ constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA pi
 #define IMGREC_I8_NT 1
 #endif
 constexpr bool kNtCodes = IMGREC_I8_NT != 0;   // non-temporal code loads in the scan
+#ifndef IMGREC_I8_PRELOAD
+#define IMGREC_I8_PRELOAD 0
+#endif
 
 
 #ifdef IMGREC_I8_STAMPS
@@ -436,6 +440,13 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     };
     Grp A, B;
     int li = wave;
+    // waves that quantise no query (wave >= nq: three of four at one query) issue their first
+    // group's code loads before the query side is ready, so HBM starts streaming during the prep
+    // (loads the prepping wave issued would queue its own query loads behind them: vmcnt is in
+    // order).  Only where the group's codes fit beside the prep's registers.
+    constexpr bool kPre = IMGREC_I8_PRELOAD && H * NBI <= 2 && NQ <= 4;
+    const bool pre = kPre && qsrc != nullptr && wave >= nq;
+    if (pre && li < cnt) load(li, A);
     __shared__ float s_qn[NQ];
     // (the 8-query instance keeps the separate prep: the fused section's registers cost its
     // VALU-bound main loop ~25 %, profiles/r05/modes_nq/)
@@ -558,7 +569,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     // (the first group's loads issued before the query prep instead measured the same:
     // profiles/r05/nq1/preload/)
     if (wave == 0) I8_STAMP(1);
-    if (li < cnt) load(li, A);
+    if (!pre && li < cnt) load(li, A);
     bool first_done = false;
     while (li < cnt) {
         if (li + kWaves < cnt) load(li + kWaves, B);
@@ -582,6 +593,41 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         }
     }
     __syncthreads();
+    if constexpr (NQ <= 4) {
+        // wave q selects query q's KM best of the 16 sorted lists at once (wave_select_sorted:
+        // the lists' leading entries bound the answer, the survivors are ranked against each
+        // other) — the round-by-round 16-lane minimum took ~5 us of dependent shuffles at the end
+        // of every workgroup (profiles/r05/i8_stamps/)
+        __shared__ uint64_t s_fold[NQ][(KM == 16 ? 64 : 128) + 192];
+        const int fq = wave;
+        if (fq >= NQ || fq >= nq) return;                // (whole waves)
+        constexpr uint64_t kEmpty = ~0ull;
+        uint64_t v[KM];
+#pragma unroll
+        for (int p = 0; p < KM; ++p) {
+            const float kk = lane < 16 ? fd[fq][lane][p] : INFINITY;
+            const int ll = lane < 16 ? fi[fq][lane][p] : -1;
+            v[p] = (ll < 0 || kk == INFINITY) ? kEmpty : ((uint64_t)key_bits_ordered(kk) << 32) | (uint32_t)ll;
+        }
+        uint64_t mine;
+        int rank;
+        const int K = wave_select_sorted<KM, (KM == 16 ? 1 : 2), 192>(v, KM, s_fold[fq], mine, rank);
+        const size_t o = (size_t)fq * ncand + (size_t)split * KM;
+        if (lane < K) {
+            cand_d[o + rank] = key_from_ordered((uint32_t)(mine >> 32));
+            cand_i[o + rank] = (int64_t)(uint32_t)mine + id_offset;
+        } else if (lane < KM) {
+            cand_d[o + lane] = INFINITY;
+            cand_i[o + lane] = -1;
+        }
+#ifdef IMGREC_I8_STAMPS
+        if (fq == 0 && lane == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            g_i8_stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
+        return;
+    }
     // wave w merges queries 4w .. 4w + 3, a 16-lane group per query, lane = list
     const int fq = wave * 4 + (lane >> 4), fl = lane & 15;
     if (fq >= NQ || fq >= nq) return;                    // (whole 16-lane groups leave together)

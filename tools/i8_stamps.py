@@ -58,7 +58,12 @@ for i in range(16):
          "wave_end_spread_median": round(float(np.median(us[:, 3:7].max(1) - us[:, 3:7].min(1))), 2),
          "fold_median": round(float(np.median(us[:, 7] - loop_end)), 2),
          "exit_last": round(float(us[:, 7].max()), 2)}
+    wg = np.where(live)[0]
+    r["loop_end_by_xcd"] = [round(float(np.median(loop_end[(wg % 8) == x])), 1) for x in range(8)]
+    r["loop_end_by_half"] = [round(float(np.median(loop_end[(wg < len(wg) // 2) == h])), 1) for h in (True, False)]
+    r["start_by_xcd"] = [round(float(np.median(us[(wg % 8) == x, 1])), 1) for x in range(8)]
     res.append(r)
     print(json.dumps(r), flush=True)
-med = {k: float(np.median([r[k] for r in res])) for k in res[0] if k not in ("cfg", "rows", "workgroups")}
+med = {k: float(np.median([r[k] for r in res])) for k in res[0]
+       if k not in ("cfg", "rows", "workgroups") and not isinstance(res[0][k], list)}
 print(json.dumps({"median_over_queries": med, "cfg": cid, "rows": rows}), flush=True)
