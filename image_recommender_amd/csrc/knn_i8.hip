@@ -45,9 +45,6 @@ constexpr int kGroup = 8;      // rows per split group (the bf16 kernels' DMA pi
 #define IMGREC_I8_NT 1
 #endif
 constexpr bool kNtCodes = IMGREC_I8_NT != 0;   // non-temporal code loads in the scan
-#ifndef IMGREC_I8_PRELOAD
-#define IMGREC_I8_PRELOAD 0
-#endif
 
 
 #ifdef IMGREC_I8_STAMPS
@@ -440,13 +437,6 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     };
     Grp A, B;
     int li = wave;
-    // waves that quantise no query (wave >= nq: three of four at one query) issue their first
-    // group's code loads before the query side is ready, so HBM starts streaming during the prep
-    // (loads the prepping wave issued would queue its own query loads behind them: vmcnt is in
-    // order).  Only where the group's codes fit beside the prep's registers.
-    constexpr bool kPre = IMGREC_I8_PRELOAD && H * NBI <= 2 && NQ <= 4;
-    const bool pre = kPre && qsrc != nullptr && wave >= nq;
-    if (pre && li < cnt) load(li, A);
     __shared__ float s_qn[NQ];
     // (the 8-query instance keeps the separate prep: the fused section's registers cost its
     // VALU-bound main loop ~25 %, profiles/r05/modes_nq/)
@@ -566,10 +556,10 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     for (int q = 0; q < NQ; ++q)      // (uniform: scalar registers, as the kernel-argument loads were)
         qn[q] = (l2 && q < nq) ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_qn[q]))) : 0.f;
 
-    // (the first group's loads issued before the query prep instead measured the same:
-    // profiles/r05/nq1/preload/)
+    // (the first group's loads issued before the query prep instead — by every wave, or only by
+    // the waves that quantise no query — measured the same: profiles/r05/nq1/preload/)
     if (wave == 0) I8_STAMP(1);
-    if (!pre && li < cnt) load(li, A);
+    if (li < cnt) load(li, A);
     bool first_done = false;
     while (li < cnt) {
         if (li + kWaves < cnt) load(li + kWaves, B);
