@@ -280,6 +280,7 @@ int create_single(int d, int metric, int device, knn_index** out) {
         ix->merge_fuse1 = *e != '0' && *e != '1';
     }
     if (const char* e = test_knob("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
+    if (const char* e = test_knob("IMGREC_CHANCE_DIRECT")) ix->chance_direct_max = std::max(0, std::atoi(e));
     if (const char* e = test_knob("IMGREC_I8_FUSED_PREP")) ix->i8_fused_prep = *e != '0';
     if (const char* e = test_knob("IMGREC_RERANK_P1")) ix->rerank_p1k = *e != '0';
     if (const char* e = test_knob("IMGREC_RERANK_NW4")) ix->rerank_nw4 = *e != '0';
@@ -308,7 +309,7 @@ void free_single(knn_index* ix) {
                     (void*)ix->mws_f, (void*)ix->stat, (void*)ix->fb_cd, (void*)ix->fb_ci,
                     (void*)ix->b16_sync,
                     (void*)ix->tail_ctl, (void*)ix->chance, (void*)ix->sc_key, (void*)ix->sc_lab,
-                    (void*)ix->sc_meta, (void*)ix->sc_done})
+                    (void*)ix->sc_meta, (void*)ix->sc_done, (void*)ix->heads})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
                     (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,

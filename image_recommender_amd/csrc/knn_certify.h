@@ -21,6 +21,12 @@ __device__ __forceinline__ bool ranks_before_r(float d1, I i1, float d2, I i2) {
 }
 
 constexpr int kRerankWaves = 8, kRerankRows = 2, kWideCap = 1024;
+// second-chance rows per wave and round (4 measured the same at config 2 and 2 us slower at
+// config 3's 1968-element rows: profiles/r05/nq1/direct/)
+#ifndef IMGREC_SC_ROWS
+#define IMGREC_SC_ROWS 2
+#endif
+constexpr int kSliceRows = IMGREC_SC_ROWS;
 static_assert(kRerankWaves == kRerankWavesHost, "host plans use kRerankWavesHost");
 
 #ifdef IMGREC_TAIL_STAMPS
@@ -206,6 +212,8 @@ struct SecondChanceLDS {
     float s_sk;
     int s_last;
     int s_flag;
+    unsigned s_heads[64];       // RerankArgs::direct: per lane, the smallest list head (key bits)
+    float s_thr;
 };
 
 // agent-scope relaxed store (global_store ... sc1): written through to where every XCD reads it
@@ -222,7 +230,8 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
     const int dp = a.dp, k = a.k, metric = a.metric, kc = a.kc, S = a.sc_slices;
     const int n4 = dp / 4;
     const float4 none[1] = {make_float4(0.f, 0.f, 0.f, 0.f)};
-    const int64_t q = item == 0 ? q_item0 : a.chance_list[item];    // item 0's: loaded at entry
+    // (item 0's query: loaded at entry; direct: item i is query i)
+    const int64_t q = a.direct ? (int64_t)item : item == 0 ? q_item0 : a.chance_list[item];
     const float* rd = a.raw_d + q * a.raw_stride_q;
     const int64_t* ri = a.raw_i + q * a.raw_stride_q;
     const int km = a.raw_km;
@@ -245,9 +254,48 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
         }
     }
     const QueryBounds B(a, q);
-    // the same prefix limit as the first pass, from the merged candidates' k-th key
-    const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
-    const float thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
+    float thr;
+    if (!a.direct) {
+        // the same prefix limit as the first pass, from the merged candidates' k-th key
+        const int nvalid = (int)__popcll(__ballot(lane < kc && a.ci[q * kc + lane] >= 0));
+        thr = nvalid >= k ? B.prefix_limit(a.cd[q * kc + k - 1]) : INFINITY;
+    } else {
+        // no merge ran: U = the k-th smallest of 64 lane minima of the lists' first keys (lane
+        // l: lists l, l + 64, ...; the scan wrote them contiguously, I8Args::heads) is >= the k-th
+        // approximate key a_k (k distinct entries are <= U), so prefix_limit(U) >= the first
+        // pass's limit and every entry that can reach the top k is still reranked (fewer than k
+        // non-empty minima: +inf, every entry)
+        if (wave == 0) {
+            constexpr int kH = 12;              // lists per lane loaded in one round (<= 768)
+            const float* hd = a.heads + q * a.raw_lists;
+            float hv[kH];
+#pragma unroll
+            for (int u = 0; u < kH; ++u) {
+                const int l = lane + 64 * u;
+                hv[u] = l < a.raw_lists ? hd[l] : INFINITY;
+            }
+            unsigned m = 0xffffffffu;
+#pragma unroll
+            for (int u = 0; u < kH; ++u)
+                if (hv[u] != INFINITY) m = min(m, key_bits_ordered(hv[u]));
+            for (int l = lane + 64 * kH; l < a.raw_lists; l += 64)
+                if (hd[l] != INFINITY) m = min(m, key_bits_ordered(hd[l]));
+            L.s_heads[lane] = m;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            int r = 0;                          // rank of (m, lane) among the 64
+#pragma unroll 8
+            for (int i = 0; i < 64; ++i) {
+                const unsigned x = L.s_heads[i];
+                r += (x < m || (x == m && i < lane)) ? 1 : 0;
+            }
+            const uint64_t hit = __ballot(m != 0xffffffffu && r == k - 1);
+            if (lane == 0)
+                L.s_thr = hit ? B.prefix_limit(key_from_ordered(L.s_heads[__builtin_ctzll(hit)])) : INFINITY;
+        }
+        __syncthreads();
+        thr = L.s_thr;
+    }
     if (t == 0) {
         L.w_n = 0;
         L.w_tau = 0xffffffffu;
@@ -275,18 +323,19 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
     int64_t* const ol_ = a.sc_lab + ((int64_t)item * S + slice) * k;
     if (!overflow) {
         const float4* q4 = reinterpret_cast<const float4*>(a.qp + q * dp);
-        for (int c0 = wave; c0 < n; c0 += NW * kRerankRows) {
-            const float4* r4[kRerankRows];
-            float acc[kRerankRows], xr[kRerankRows];
+        // kSliceRows rows per wave and round (the rows' keys have the same bits whatever the count)
+        for (int c0 = wave; c0 < n; c0 += NW * kSliceRows) {
+            const float4* r4[kSliceRows];
+            float acc[kSliceRows], xr[kSliceRows];
 #pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
+            for (int v = 0; v < kSliceRows; ++v) {
                 const int64_t row = L.w_lab[min(c0 + NW * v, n - 1)] - a.id_offset;
                 r4[v] = reinterpret_cast<const float4*>(a.xb + row * dp);
                 xr[v] = a.xn[row];                      // loaded with the row, not after it
             }
-            rerank_dots<0>(q4, none, n4, lane, r4, acc);
+            rerank_dots<0, kSliceRows>(q4, none, n4, lane, r4, acc);
 #pragma unroll
-            for (int v = 0; v < kRerankRows; ++v) {
+            for (int v = 0; v < kSliceRows; ++v) {
                 const int c = c0 + NW * v;
                 if (lane == 0 && c < n) L.w_key[c] = rerank_key(acc[v], B.qn, xr[v], metric);
             }

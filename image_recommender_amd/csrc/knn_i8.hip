@@ -283,7 +283,8 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
                    int nsplit, int64_t id_offset, int l2, float* __restrict__ cand_d,
                    int64_t* __restrict__ cand_i, int ncand, const float* __restrict__ qsrc, int d,
                    int dp, int normalize, float* __restrict__ qpad, float* __restrict__ qnorm_out,
-                   float* __restrict__ qresid) {
+                   float* __restrict__ qresid, int* __restrict__ zero_ctl,
+                   float* __restrict__ heads) {
     // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
     // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
     // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
@@ -305,6 +306,8 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     const int j = lane & 15, g = lane >> 4;
     const int64_t rowb = i8_row_bytes(nblk);
     if (wave == 0) I8_STAMP(0);
+    // the certificate tail's claim counters, when no rerank launch runs between (I8Args::zero_ctl)
+    if (zero_ctl && split == 0 && tid < 4) zero_ctl[tid] = 0;
     float qn[NQ];
     float kd[KM];
     int ki[KM];
@@ -606,10 +609,12 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         if (lane < K) {
             cand_d[o + rank] = key_from_ordered((uint32_t)(mine >> 32));
             cand_i[o + rank] = (int64_t)(uint32_t)mine + id_offset;
+            if (heads && rank == 0) heads[(size_t)fq * nsplit + split] = key_from_ordered((uint32_t)(mine >> 32));
         } else if (lane < KM) {
             cand_d[o + lane] = INFINITY;
             cand_i[o + lane] = -1;
         }
+        if (heads && K == 0 && lane == 0) heads[(size_t)fq * nsplit + split] = INFINITY;
 #ifdef IMGREC_I8_STAMPS
         if (fq == 0 && lane == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -641,6 +646,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
             const size_t o = (size_t)fq * ncand + (size_t)split * KM + p;
             cand_d[o] = bk;
             cand_i[o] = bk == INFINITY ? (int64_t)-1 : (int64_t)bl + id_offset;
+            if (heads && p == 0) heads[(size_t)fq * nsplit + split] = bk;
         }
     }
 #ifdef IMGREC_I8_STAMPS
@@ -692,7 +698,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
                        a.xnorm, a.nrows, a.nblk, a.qcodes, a.qscales, a.qnorm, a.nq, a.nsplit,      \
                        a.id_offset,                                                                 \
                        a.l2, a.cand_d, a.cand_i, a.ncand, a.qsrc, a.d, a.dp, a.normalize, a.qpad,  \
-                       a.qnorm_out, a.qresid)
+                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads)
 #define IMGREC_I8_NBI(NQV, KMV)                                   \
     do {                                                          \
         switch (nbi) {                                            \

@@ -102,6 +102,10 @@ struct knn_index {
     int i8_wgpcu = imgrec::kI8WGPCUDefault;
     bool merge_fuse = true;
     bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
+    // int8 batches of at most this many queries skip the merge and the first rerank: the
+    // certificate tail's second chance answers every query (RerankArgs::direct);
+    // IMGREC_CHANCE_DIRECT=N sets it, 0 = off
+    int chance_direct_max = 1;
     bool stream_lists = true;   // exact lists of <= 4 queries from one fp32 stream (IMGREC_STREAM_LISTS=0: tiles)
     bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
     bool rerank_nw4 = false;    // IMGREC_RERANK_NW4=1: large batches rerank on 4-wave workgroups
@@ -163,6 +167,7 @@ struct knn_index {
     uint16_t* qb16 = nullptr; size_t qb16_cap = 0;
     float* q_resid = nullptr; size_t q_resid_cap = 0;
     float* floor = nullptr; size_t floor_cap = 0;
+    float* heads = nullptr; size_t heads_cap = 0;       // int8 lists' first keys (direct route)
     float* mws_d = nullptr; size_t mws_d_cap = 0;          // two-level candidate merge workspace
     int64_t* mws_i = nullptr; size_t mws_i_cap = 0;
     float* mws_f = nullptr; size_t mws_f_cap = 0;

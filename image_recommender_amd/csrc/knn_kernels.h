@@ -88,6 +88,11 @@ struct RerankArgs {
                                 // large batches use k: their rerank is bound by row bytes
     int chance_skip = 0;        // queue a query whose band certainly-ish exceeds K' straight to the
                                 // second chance (no first-pass row reads); needs raw_d
+    int direct = 0;             // no merge and no rerank launch: the certificate tail gives EVERY
+                                // query (item i = query i) the second chance, its prefix limit from
+                                // the raw lists' first keys at heads + q * raw_lists (I8Args::heads;
+                                // cd / ci / floor / chance_list unused)
+    const float* heads = nullptr;
     float* D;
     int64_t* I;
     int* stats;                 // this chunk's device counters (zero on entry): [0] queries left
@@ -214,6 +219,13 @@ struct I8Args {
     float* qpad;
     float* qnorm_out;
     float* qresid;
+    // non-NULL: workgroup 0 zeroes these 4 ints (the certificate tail's claim counters, which
+    // the rerank launch zeroes otherwise — RerankArgs::direct has none)
+    int* zero_ctl = nullptr;
+    // non-NULL: per (query, split) the first key of the split's list (+inf: empty) at
+    // heads[q * nsplit + split] — the direct second chance's prefix-limit bound, 4 B per list
+    // instead of a strided read of every list's first entry
+    float* heads = nullptr;
 };
 // Bytes per row of the int8 copy: 64 per block, no padding (round 4; rows were whole 1-KiB
 // groups of 16 blocks, 25 % zeros at d = 768).  Blocks sit in groups of 16 (the scan's 16 lanes of

@@ -681,7 +681,8 @@ __device__ __forceinline__ void merge_query_wave(const float* __restrict__ cd,
 //   3. exact (2,1)-tile items (query block, row split) are claimed from ctl[3]; the workgroup
 //      that finishes a query block's last split merges that block's lists into the rows
 //      fail_list[q] of D / I.
-// ctl[0..3] are zeroed by the rerank kernel (the launch before this one on the stream).
+// ctl[0..3] are zeroed by the rerank kernel (the launch before this one on the stream; with
+// RerankArgs::direct, by the candidate scan, and every query is a second-chance item).
 // ---------------------------------------------------------------------------------------------
 constexpr int kTailWR = 2, kTailNS = 3, kTailBK = 16, kTailWB = 4, kTailWaves = kTailWR;
 
@@ -697,8 +698,9 @@ cert_tail_kernel(const TailArgs a) {
     int* const sp = a.stat + 4 * a.parity;
     int* const ctl = a.r.tail_ctl;
     TAIL_STAMP(0);
-    const int n_chance = sp[3];                 // final: the rerank kernel has completed
-    const int q_item0 = a.r.chance_list ? a.r.chance_list[0] : -1;   // in the same round trip
+    // final: the rerank kernel has completed (direct: no rerank ran, every query is an item)
+    const int n_chance = a.r.direct ? (int)a.r.nq : sp[3];
+    const int q_item0 = !a.r.direct && a.r.chance_list ? a.r.chance_list[0] : -1;   // same round trip
     if (n_chance == 0 && sp[0] == 0) {          // the common case: every query certified
         if (blockIdx.x == 0 && t == 0) {
             int* acc = a.stat + 8;
@@ -714,14 +716,23 @@ cert_tail_kernel(const TailArgs a) {
     bool planner = false;
     int known = -1;                             // the re-run count, when the planner knows it
     if (n_chance > 0) {
-        // units = (item, slice), claimed from ctl[0]; the workgroup that finishes an item's last
-        // slice counts the item in ctl[1]
+        // units = (item, slice): workgroup b takes unit b, then (only when the units outnumber
+        // the grid) claims grid + ctl[0]++ — the grid's first claims all on one address
+        // serialised ~3 us of a one-query tail; the workgroup that finishes an item's last slice
+        // counts the item in ctl[1]
         const int S = a.r.sc_slices;
+        bool first_unit = true;
         for (;;) {
-            if (t == 0) s_val = __hip_atomic_fetch_add(ctl + 0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __syncthreads();
-            const int unit = s_val;
-            __syncthreads();
+            int unit = (int)blockIdx.x;
+            if (!first_unit) {
+                if ((int)gridDim.x >= n_chance * S) break;     // every unit was a first one
+                if (t == 0)
+                    s_val = (int)gridDim.x + __hip_atomic_fetch_add(ctl + 0, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __syncthreads();
+                unit = s_val;
+                __syncthreads();
+            }
+            first_unit = false;
             TAIL_STAMP(1);
             if (unit >= n_chance * S) break;
             const int res = second_chance_slice<kTailWaves>(a.r, unit / S, unit % S,
@@ -760,9 +771,10 @@ cert_tail_kernel(const TailArgs a) {
         if (count > 0) wg_release_stores();     // this workgroup's fail_list stores (one item)
         if (t == 0) {
             int* acc = a.stat + 8;
+            const int first_fail = a.r.direct ? (int)a.r.nq : sp[2];   // direct: all had no first pass
             acc[0] = a.first ? count : acc[0] + count;
             acc[1] = a.first ? sp[1] : max(acc[1], sp[1]);
-            acc[2] = a.first ? sp[2] : acc[2] + sp[2];
+            acc[2] = a.first ? first_fail : acc[2] + first_fail;
             int* other = a.stat + 4 * (a.parity ^ 1);
             other[0] = 0; other[1] = 0; other[2] = 0; other[3] = 0;
         }

@@ -166,7 +166,7 @@ int certify_chunk(knn_index* ix, RerankArgs& r, const float* qpad, const float* 
     // opt-in (IMGREC_RERANK_NW4=1) — measured 3-4 us slower per 125k-row step than 8 waves, the
     // rerank is not residency-bound (profiles/r05/rerank_nw4_ab/)
     r.nw = ix->rerank_nw4 && nq > ix->cus && r.l1_G == 0 && r.s_lists == 0 && !r.chance_skip ? 4 : 0;
-    KNN_HIP(launch_rerank_certify(r, st));
+    if (!r.direct) KNN_HIP(launch_rerank_certify(r, st));
     TailArgs t{};
     t.r = r;
     t.parity = parity;
@@ -343,11 +343,35 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
     a.km = p.km;
     a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
     a.cand_i = ix->cand_i; a.ncand = p.ncand;
+    // direct: no merge, no rerank launch — the certificate tail reranks every query's list entries
+    // under its prefix limit (RerankArgs::direct); the scan zeroes the tail's claim counters
+    const bool direct = ix->chance_direct_max > 0 && nq <= ix->chance_direct_max && k <= 64;
+    if (direct) {
+        if ((rc = grow(&ix->tail_ctl, &ix->tail_ctl_cap, (size_t)4 + round_up(nq, 32) / 32)) != KNN_OK)
+            return rc;
+        a.zero_ctl = ix->tail_ctl;
+        if ((rc = grow(&ix->heads, &ix->heads_cap, (size_t)nq * p.nsplit)) != KNN_OK) return rc;
+        a.heads = ix->heads;
+    }
     hipEvent_t e1 = nullptr;
     if (timed && (rc = timed_begin(ix, st, &e1)) != KNN_OK) return rc;
     KNN_HIP(launch_i8_scan(a, st));
     if (e1) KNN_HIP(hipEventRecord(e1, st));
     const int nlists = p.nsplit, ngrp = (nlists + 63) / 64;
+    if (direct) {
+        RerankArgs r{};
+        r.mode = kModeI8;
+        r.qp = qpad; r.qnorm = qnorm; r.dp = ix->dp; r.xb = ix->xb; r.xn = ix->xn;
+        r.xn_max = ix->xn_max; r.id_offset = ix->id_offset;
+        r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = i8_acc_coef(ix->nblk8);
+        r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
+        r.q_resid = ix->q8r; r.xr_max = ix->x8r_max;
+        r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = p.km;
+        r.raw_stride_q = p.ncand;
+        r.direct = 1;
+        r.heads = ix->heads;
+        return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
+    }
     if (ngrp > 1) {
         if ((rc = grow(&ix->mws_d, &ix->mws_d_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;
         if ((rc = grow(&ix->mws_i, &ix->mws_i_cap, (size_t)nq * ngrp * kc)) != KNN_OK) return rc;

@@ -277,3 +277,58 @@ def test_i8_fused_query_prep_matches_its_own_launch(faiss, monkeypatch, d, metri
     # (at d >= 1024 the mixture's neighbours crowd inside the rigorous window, as in
     # test_i8_l2_shapes: the tight check there, the identity with the separate launch here)
     check_knn(D1, I1, xb, xq, 10, metric, min_exact_frac=0.5 if d < 1024 else 0.25)
+
+
+@pytest.mark.parametrize("d", [64, 300, 768, 1968])
+@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
+def test_i8_direct_second_chance_matches_first_pass_route(faiss, monkeypatch, d, metric):
+    """One-query int8 searches skip the merge and the first rerank (RerankArgs::direct, round 5):
+    the certificate tail reranks every list entry under a prefix limit taken from the lists' heads
+    and certifies against the list floor.  The returned bits equal the first-pass route's
+    (IMGREC_CHANCE_DIRECT=0) whenever neither route needed the exact re-run, for 1-4 queries
+    (=4: several second-chance items, the planner picked by the item count); the oracle checks
+    both."""
+    xb = mixture(20011, d, centres=40, seed=d + 17)
+    xq = mixture(4, d, centres=40, seed=d + 18)
+    idx = {}
+    for name, env in (("first_pass", "0"), ("direct", "4")):
+        monkeypatch.setenv("IMGREC_CHANCE_DIRECT", env)
+        idx[name] = _index(faiss, d, metric)          # (the knob is read at index creation)
+        monkeypatch.delenv("IMGREC_CHANCE_DIRECT")
+        idx[name].add(xb)
+        idx[name].search_mode = "i8"
+    for nq in (1, 2, 4):
+        q = np.ascontiguousarray(xq[:nq])
+        D0, I0 = idx["first_pass"].search(q, 10)
+        r0 = _stats(idx["first_pass"], nq)
+        D1, I1 = idx["direct"].search(q, 10)
+        r1 = _stats(idx["direct"], nq)
+        st = idx["direct"].certificate_stats()
+        assert st["second_chance"] + st["exact_reruns"] == nq, st     # every query took it
+        if r0 == 0 and r1 == 0:
+            assert np.array_equal(I1, I0), (nq, np.argwhere(I1 != I0)[:5])
+            assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), nq
+        check_knn(D1, I1, xb, q, 10, metric, min_exact_frac=0.5 if d < 1024 else 0.25)
+
+
+def test_i8_direct_route_exact_rerun_of_crowded_queries(faiss, monkeypatch):
+    """Single queries whose nearest row has 12000 copies (rows of 8-row groups interleaved over
+    the 512 splits: ~24 copies per split, more than its list of 16 holds, so every list ends in
+    ties and the list floor cannot certify): the direct route's second chance fails and the
+    device-planned exact re-run answers each, ties by the smaller label."""
+    monkeypatch.setenv("IMGREC_CHANCE_DIRECT", "4")
+    idx = faiss.IndexFlatL2(256)
+    monkeypatch.delenv("IMGREC_CHANCE_DIRECT")
+    dup = 12000
+    base = mixture(4, 256, centres=4, seed=3)
+    xb = np.concatenate([np.repeat(base, dup, axis=0), mixture(9000, 256, centres=8, seed=4)])
+    idx.add(xb)
+    idx.search_mode = "i8"
+    src = np.array([0, 1, 2, 3])
+    for nq in (1, 4):
+        xq = base[src[:nq]] + np.float32(1e-3)
+        D, I = idx.search(xq, 10)
+        st = idx.certificate_stats()
+        assert st["candidate_queries"] == nq and st["exact_reruns"] == nq, st
+        assert (I == src[:nq, None] * dup + np.arange(10)[None, :]).all()
+        check_knn(D, I, xb, xq, 10, "l2")

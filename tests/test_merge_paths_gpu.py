@@ -12,7 +12,8 @@ sent straight to the second chance by its band) and IMGREC_I8_FUSED_PREP=0 (the 
 from their own launch instead of inside the scan) and IMGREC_RERANK_P1=0 (a 16-row first rerank
 phase for every batch instead of k rows past one rerank workgroup per CU) and
 IMGREC_MERGE_SINGLE=1 (the single-level merge of <= 64 lists inside the rerank workgroup) and
-IMGREC_RERANK_NW4=1 (4-wave rerank workgroups for large batches)
+IMGREC_RERANK_NW4=1 (4-wave rerank workgroups for large batches) and IMGREC_CHANCE_DIRECT=0 (one-query
+int8 searches through the merge and the first rerank instead of straight to the second chance)
 bit for bit, and the default against the float64 oracle (tests/knn_check.py).  The config-2
 distribution (bench.py's 1M x 768 rows) makes most single queries take the second
 chance, so the tail's hand-offs run under every route.
@@ -56,7 +57,8 @@ VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "level2only": {"IMGREC_MERGE_
             "wgpcu1": {"IMGREC_I8_WGPCU": "1"},
             "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"},
             "separate_prep": {"IMGREC_I8_FUSED_PREP": "0"}, "rerank_p1_16": {"IMGREC_RERANK_P1": "0"},
-            "single_fused": {"IMGREC_MERGE_SINGLE": "1"}, "rerank_nw4": {"IMGREC_RERANK_NW4": "1"}}
+            "single_fused": {"IMGREC_MERGE_SINGLE": "1"}, "rerank_nw4": {"IMGREC_RERANK_NW4": "1"},
+            "first_pass": {"IMGREC_CHANCE_DIRECT": "0"}}
 
 
 @pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257, 1024])

@@ -62,6 +62,9 @@ for i in range(16):
     r["loop_end_by_xcd"] = [round(float(np.median(loop_end[(wg % 8) == x])), 1) for x in range(8)]
     r["loop_end_by_half"] = [round(float(np.median(loop_end[(wg < len(wg) // 2) == h])), 1) for h in (True, False)]
     r["start_by_xcd"] = [round(float(np.median(us[(wg % 8) == x, 1])), 1) for x in range(8)]
+    r["loop_end_pct"] = [round(float(np.percentile(loop_end, p)), 1) for p in (0, 5, 25, 50, 75, 95, 100)]
+    if os.environ.get("DUMP"):               # per workgroup: id, query side ready, loop end (us)
+        np.save(f"{os.environ['DUMP']}_q{i}.npy", np.stack([wg, us[:, 1], loop_end]))
     res.append(r)
     print(json.dumps(r), flush=True)
 med = {k: float(np.median([r[k] for r in res])) for k in res[0]
