@@ -240,7 +240,9 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
     auto entry = [&](int j) { return (slice + (j / km) * S) * km + j % km; };
     // the slice's first kPre entries per thread are loaded together with the bounds' inputs (one
     // dependent round trip instead of two; a one-query second chance is a chain of them)
-    constexpr int kPre = 4;
+    // (16 measured the same at config 2's 2048 entries per slice of unfolded lists and 0.6 us
+    // slower at config 3: profiles/r05/nq1/direct_raw/)
+    constexpr int kPre = 8;
     float pv[kPre];
     int64_t pl[kPre];
 #pragma unroll
@@ -267,18 +269,19 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
         // non-empty minima: +inf, every entry)
         if (wave == 0) {
             constexpr int kH = 12;              // lists per lane loaded in one round (<= 768)
-            const float* hd = a.heads + q * a.raw_lists;
+            const int nh = a.heads_n > 0 ? a.heads_n : a.raw_lists;
+            const float* hd = a.heads + q * nh;
             float hv[kH];
 #pragma unroll
             for (int u = 0; u < kH; ++u) {
                 const int l = lane + 64 * u;
-                hv[u] = l < a.raw_lists ? hd[l] : INFINITY;
+                hv[u] = l < nh ? hd[l] : INFINITY;
             }
             unsigned m = 0xffffffffu;
 #pragma unroll
             for (int u = 0; u < kH; ++u)
                 if (hv[u] != INFINITY) m = min(m, key_bits_ordered(hv[u]));
-            for (int l = lane + 64 * kH; l < a.raw_lists; l += 64)
+            for (int l = lane + 64 * kH; l < nh; l += 64)
                 if (hd[l] != INFINITY) m = min(m, key_bits_ordered(hd[l]));
             L.s_heads[lane] = m;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -314,7 +317,19 @@ __device__ __forceinline__ int second_chance_slice(const RerankArgs& a, int item
 #pragma unroll
     for (int u = 0; u < kPre; ++u)
         if (t + u * NT < ne) take(t + u * NT, pl[u], pv[u]);
-    for (int j = t + kPre * NT; j < ne; j += NT) take(j, ri[entry(j)], rd[entry(j)]);
+    // the rest in batches of kPre loads per thread (the direct route's unfolded lists: up to
+    // 2048 entries per slice)
+    for (int j0 = t + kPre * NT; j0 < ne; j0 += kPre * NT) {
+#pragma unroll
+        for (int u = 0; u < kPre; ++u) {
+            const int j = j0 + u * NT;
+            pl[u] = j < ne ? ri[entry(j)] : -1;
+            pv[u] = j < ne ? rd[entry(j)] : INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < kPre; ++u)
+            if (j0 + u * NT < ne) take(j0 + u * NT, pl[u], pv[u]);
+    }
     __syncthreads();
     TAIL_STAMP(2);
     const int n = L.w_n;

@@ -284,7 +284,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
                    int64_t* __restrict__ cand_i, int ncand, const float* __restrict__ qsrc, int d,
                    int dp, int normalize, float* __restrict__ qpad, float* __restrict__ qnorm_out,
                    float* __restrict__ qresid, int* __restrict__ zero_ctl,
-                   float* __restrict__ heads) {
+                   float* __restrict__ heads, int raw16) {
     // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
     // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
     // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
@@ -587,6 +587,26 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     }
     __syncthreads();
     if constexpr (NQ <= 4) {
+        if (raw16) {
+            // the direct route (I8Args::raw16): the split's 16 sorted lane lists go out unfolded
+            // (list l of the split = 16 split + l), and wave q writes the smallest of their first
+            // keys as the split's head — the fold's ~5 us at the end of the last workgroup leave
+            // the critical path; the second chance filters 16x the entries instead
+            for (int i = tid; i < nq * 16 * KM; i += kWaves * 64) {
+                const int qi = i / (16 * KM), r = i - qi * (16 * KM);
+                const int ll = fi[qi][r / KM][r % KM];
+                const size_t o = (size_t)qi * ncand + (size_t)split * 16 * KM + r;
+                cand_d[o] = ll < 0 ? INFINITY : fd[qi][r / KM][r % KM];
+                cand_i[o] = ll < 0 ? (int64_t)-1 : (int64_t)ll + id_offset;
+            }
+            if (heads && wave < nq) {
+                float h = lane < 16 && fi[wave][lane][0] >= 0 ? fd[wave][lane][0] : INFINITY;
+#pragma unroll
+                for (int off = 8; off > 0; off >>= 1) h = fminf(h, __shfl_xor(h, off, 64));
+                if (lane == 0) heads[(size_t)wave * nsplit + split] = h;
+            }
+            return;
+        }
         // wave q selects query q's KM best of the 16 sorted lists at once (wave_select_sorted:
         // the lists' leading entries bound the answer, the survivors are ranked against each
         // other) — the round-by-round 16-lane minimum took ~5 us of dependent shuffles at the end
@@ -691,6 +711,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
                    !a.qnorm_out || !a.qresid))
         return hipErrorInvalidValue;
     if (!a.qsrc && (!a.qcodes || !a.qscales || !a.qnorm)) return hipErrorInvalidValue;
+    if (a.raw16 && (a.nq > 4 || a.ncand < a.nsplit * 16 * a.km)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);
     const int nbi = (a.nblk + 15) / 16;
 #define IMGREC_I8(NQV, KMV, NBIV)                                                                 \
@@ -698,7 +719,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
                        a.xnorm, a.nrows, a.nblk, a.qcodes, a.qscales, a.qnorm, a.nq, a.nsplit,      \
                        a.id_offset,                                                                 \
                        a.l2, a.cand_d, a.cand_i, a.ncand, a.qsrc, a.d, a.dp, a.normalize, a.qpad,  \
-                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads)
+                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads, a.raw16)
 #define IMGREC_I8_NBI(NQV, KMV)                                   \
     do {                                                          \
         switch (nbi) {                                            \

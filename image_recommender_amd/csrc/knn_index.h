@@ -106,6 +106,9 @@ struct knn_index {
     // certificate tail's second chance answers every query (RerankArgs::direct);
     // IMGREC_CHANCE_DIRECT=N sets it, 0 = off
     int chance_direct_max = 1;
+    // ... over the scan's lane lists unfolded: 1 = while <= 4096 per query, 2 = always, 0 = never
+    // (IMGREC_DIRECT_RAW)
+    int direct_raw = 1;
     bool stream_lists = true;   // exact lists of <= 4 queries from one fp32 stream (IMGREC_STREAM_LISTS=0: tiles)
     bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
     bool rerank_nw4 = false;    // IMGREC_RERANK_NW4=1: large batches rerank on 4-wave workgroups

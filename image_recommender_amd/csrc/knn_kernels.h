@@ -93,6 +93,7 @@ struct RerankArgs {
                                 // the raw lists' first keys at heads + q * raw_lists (I8Args::heads;
                                 // cd / ci / floor / chance_list unused)
     const float* heads = nullptr;
+    int heads_n = 0;            // first keys per query at heads (raw_lists when 0)
     float* D;
     int64_t* I;
     int* stats;                 // this chunk's device counters (zero on entry): [0] queries left
@@ -226,6 +227,9 @@ struct I8Args {
     // heads[q * nsplit + split] — the direct second chance's prefix-limit bound, 4 B per list
     // instead of a strided read of every list's first entry
     float* heads = nullptr;
+    // <= 4 queries: the split's 16 lane lists written unfolded (16 nsplit lists of km per query;
+    // ncand >= 16 nsplit km) and heads = the smallest of their first keys — the direct route
+    int raw16 = 0;
 };
 // Bytes per row of the int8 copy: 64 per block, no padding (round 4; rows were whole 1-KiB
 // groups of 16 blocks, 25 % zeros at d = 768).  Blocks sit in groups of 16 (the scan's 16 lanes of

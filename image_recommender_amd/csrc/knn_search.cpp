@@ -318,11 +318,21 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     const int kc = kB16Cand;
     const Plan p = make_i8_plan(ix->ntotal, nq, k, ix->cus, ix->i8_wgpcu, ix->nblk8);
+    // direct: no merge, no rerank launch — the certificate tail reranks every query's list entries
+    // under its prefix limit (RerankArgs::direct); the scan zeroes the tail's claim counters and
+    // (raw: <= 4 queries) writes its 16 lane lists per split unfolded
+    const bool direct = ix->chance_direct_max > 0 && nq <= ix->chance_direct_max && k <= 64;
+    // (unfolded while they make <= 4096 lists per query, i.e. <= 1024 entries per second-chance
+    // slice: config 3's 256 splits 2 us faster, config 2's 512 splits 1 us slower than folded,
+    // profiles/r05/nq1/direct_raw/; IMGREC_DIRECT_RAW=2: unfolded at any split count)
+    const bool raw = direct && nq <= 4 &&
+                     (ix->direct_raw == 2 || (ix->direct_raw == 1 && 16 * p.nsplit <= 4096));
+    const int ncand = raw ? p.nsplit * 16 * p.km : p.ncand;
     int rc;
     if ((rc = ensure_i8(ix, st)) != KNN_OK) return rc;
     if ((rc = refresh_maxima(ix, st)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
-    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * p.ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)nq * ncand)) != KNN_OK) return rc;
+    if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)nq * ncand)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_d, &ix->cand2_d_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->cand2_i, &ix->cand2_i_cap, (size_t)nq * kc)) != KNN_OK) return rc;
     if ((rc = grow(&ix->floor, &ix->floor_cap, (size_t)nq)) != KNN_OK) return rc;
@@ -342,10 +352,7 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
     }
     a.km = p.km;
     a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
-    a.cand_i = ix->cand_i; a.ncand = p.ncand;
-    // direct: no merge, no rerank launch — the certificate tail reranks every query's list entries
-    // under its prefix limit (RerankArgs::direct); the scan zeroes the tail's claim counters
-    const bool direct = ix->chance_direct_max > 0 && nq <= ix->chance_direct_max && k <= 64;
+    a.cand_i = ix->cand_i; a.ncand = ncand; a.raw16 = raw ? 1 : 0;
     if (direct) {
         if ((rc = grow(&ix->tail_ctl, &ix->tail_ctl_cap, (size_t)4 + round_up(nq, 32) / 32)) != KNN_OK)
             return rc;
@@ -366,10 +373,12 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
         r.kc = kc; r.nq = nq; r.k = k; r.metric = kmetric; r.c_split = i8_acc_coef(ix->nblk8);
         r.c_fp = rerank_coef(ix->dp); r.D = D; r.I = I;
         r.q_resid = ix->q8r; r.xr_max = ix->x8r_max;
-        r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = nlists; r.raw_km = p.km;
-        r.raw_stride_q = p.ncand;
+        r.raw_d = ix->cand_d; r.raw_i = ix->cand_i; r.raw_lists = raw ? 16 * nlists : nlists;
+        r.raw_km = p.km;
+        r.raw_stride_q = ncand;
         r.direct = 1;
         r.heads = ix->heads;
+        r.heads_n = nlists;
         return certify_chunk(ix, r, qpad, qnorm, nq, k, D, I, st, first);
     }
     if (ngrp > 1) {

@@ -284,51 +284,66 @@ def test_i8_fused_query_prep_matches_its_own_launch(faiss, monkeypatch, d, metri
 def test_i8_direct_second_chance_matches_first_pass_route(faiss, monkeypatch, d, metric):
     """One-query int8 searches skip the merge and the first rerank (RerankArgs::direct, round 5):
     the certificate tail reranks every list entry under a prefix limit taken from the lists' heads
-    and certifies against the list floor.  The returned bits equal the first-pass route's
+    and certifies against the list floor — over the scan's 16 unfolded lane lists per split
+    (IMGREC_DIRECT_RAW=2; the default unfolds them up to 256 splits) or the folded list (=0).  The returned bits equal the first-pass route's
     (IMGREC_CHANCE_DIRECT=0) whenever neither route needed the exact re-run, for 1-4 queries
     (=4: several second-chance items, the planner picked by the item count); the oracle checks
     both."""
     xb = mixture(20011, d, centres=40, seed=d + 17)
     xq = mixture(4, d, centres=40, seed=d + 18)
     idx = {}
-    for name, env in (("first_pass", "0"), ("direct", "4")):
-        monkeypatch.setenv("IMGREC_CHANCE_DIRECT", env)
-        idx[name] = _index(faiss, d, metric)          # (the knob is read at index creation)
-        monkeypatch.delenv("IMGREC_CHANCE_DIRECT")
+    for name, env in (("first_pass", {"IMGREC_CHANCE_DIRECT": "0"}),
+                      ("direct", {"IMGREC_CHANCE_DIRECT": "4", "IMGREC_DIRECT_RAW": "2"}),
+                      ("direct_folded", {"IMGREC_CHANCE_DIRECT": "4", "IMGREC_DIRECT_RAW": "0"})):
+        for k_, v in env.items():
+            monkeypatch.setenv(k_, v)
+        idx[name] = _index(faiss, d, metric)          # (the knobs are read at index creation)
+        for k_ in env:
+            monkeypatch.delenv(k_)
         idx[name].add(xb)
         idx[name].search_mode = "i8"
     for nq in (1, 2, 4):
         q = np.ascontiguousarray(xq[:nq])
         D0, I0 = idx["first_pass"].search(q, 10)
         r0 = _stats(idx["first_pass"], nq)
-        D1, I1 = idx["direct"].search(q, 10)
-        r1 = _stats(idx["direct"], nq)
-        st = idx["direct"].certificate_stats()
-        assert st["second_chance"] + st["exact_reruns"] == nq, st     # every query took it
-        if r0 == 0 and r1 == 0:
-            assert np.array_equal(I1, I0), (nq, np.argwhere(I1 != I0)[:5])
-            assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), nq
-        check_knn(D1, I1, xb, q, 10, metric, min_exact_frac=0.5 if d < 1024 else 0.25)
+        for name in ("direct", "direct_folded"):
+            D1, I1 = idx[name].search(q, 10)
+            r1 = _stats(idx[name], nq)
+            st = idx[name].certificate_stats()
+            assert st["second_chance"] + st["exact_reruns"] == nq, st     # every query took it
+            if r0 == 0 and r1 == 0:
+                assert np.array_equal(I1, I0), (name, nq, np.argwhere(I1 != I0)[:5])
+                assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), (name, nq)
+            check_knn(D1, I1, xb, q, 10, metric, min_exact_frac=0.5 if d < 1024 else 0.25)
 
 
 def test_i8_direct_route_exact_rerun_of_crowded_queries(faiss, monkeypatch):
     """Single queries whose nearest row has 12000 copies (rows of 8-row groups interleaved over
-    the 512 splits: ~24 copies per split, more than its list of 16 holds, so every list ends in
-    ties and the list floor cannot certify): the direct route's second chance fails and the
-    device-planned exact re-run answers each, ties by the smaller label."""
-    monkeypatch.setenv("IMGREC_CHANCE_DIRECT", "4")
-    idx = faiss.IndexFlatL2(256)
-    monkeypatch.delenv("IMGREC_CHANCE_DIRECT")
+    the 512 splits: ~24 copies per split).  Over the folded lists (IMGREC_DIRECT_RAW=0) more than a
+    list of 16 holds, so every list ends in ties, the list floor cannot certify, the direct
+    route's second chance fails and the device-planned exact re-run answers each.  Over the 16
+    unfolded lane lists per split (=2) every copy is a candidate and the second chance settles
+    it.  Either way the ten smallest labels come back."""
     dup = 12000
     base = mixture(4, 256, centres=4, seed=3)
     xb = np.concatenate([np.repeat(base, dup, axis=0), mixture(9000, 256, centres=8, seed=4)])
-    idx.add(xb)
-    idx.search_mode = "i8"
     src = np.array([0, 1, 2, 3])
-    for nq in (1, 4):
-        xq = base[src[:nq]] + np.float32(1e-3)
-        D, I = idx.search(xq, 10)
-        st = idx.certificate_stats()
-        assert st["candidate_queries"] == nq and st["exact_reruns"] == nq, st
-        assert (I == src[:nq, None] * dup + np.arange(10)[None, :]).all()
-        check_knn(D, I, xb, xq, 10, "l2")
+    for raw in ("0", "2"):
+        monkeypatch.setenv("IMGREC_CHANCE_DIRECT", "4")
+        monkeypatch.setenv("IMGREC_DIRECT_RAW", raw)
+        idx = faiss.IndexFlatL2(256)
+        monkeypatch.delenv("IMGREC_CHANCE_DIRECT")
+        monkeypatch.delenv("IMGREC_DIRECT_RAW")
+        idx.add(xb)
+        idx.search_mode = "i8"
+        for nq in (1, 4):
+            xq = base[src[:nq]] + np.float32(1e-3)
+            D, I = idx.search(xq, 10)
+            st = idx.certificate_stats()
+            if raw == "0":      # folded lists end in ties: only the exact re-run settles them
+                assert st["candidate_queries"] == nq and st["exact_reruns"] == nq, st
+            else:               # the 16 lane lists per split hold every copy (~1.5 each)
+                assert st["second_chance"] + st["exact_reruns"] == nq, st
+            assert (I == src[:nq, None] * dup + np.arange(10)[None, :]).all(), (raw, nq)
+            check_knn(D, I, xb, xq, 10, "l2")
+        del idx

@@ -13,7 +13,9 @@ from their own launch instead of inside the scan) and IMGREC_RERANK_P1=0 (a 16-r
 phase for every batch instead of k rows past one rerank workgroup per CU) and
 IMGREC_MERGE_SINGLE=1 (the single-level merge of <= 64 lists inside the rerank workgroup) and
 IMGREC_RERANK_NW4=1 (4-wave rerank workgroups for large batches) and IMGREC_CHANCE_DIRECT=0 (one-query
-int8 searches through the merge and the first rerank instead of straight to the second chance)
+int8 searches through the merge and the first rerank instead of straight to the second chance) and
+IMGREC_DIRECT_RAW=2 (that second chance over the scan's 16 unfolded lane lists per split, which the
+default uses only up to 256 splits)
 bit for bit, and the default against the float64 oracle (tests/knn_check.py).  The config-2
 distribution (bench.py's 1M x 768 rows) makes most single queries take the second
 chance, so the tail's hand-offs run under every route.
@@ -58,7 +60,7 @@ VARIANTS = {"unfused": {"IMGREC_MERGE_FUSE": "0"}, "level2only": {"IMGREC_MERGE_
             "wgpcu5": {"IMGREC_I8_WGPCU": "5"}, "noskip": {"IMGREC_CHANCE_SKIP": "0"},
             "separate_prep": {"IMGREC_I8_FUSED_PREP": "0"}, "rerank_p1_16": {"IMGREC_RERANK_P1": "0"},
             "single_fused": {"IMGREC_MERGE_SINGLE": "1"}, "rerank_nw4": {"IMGREC_RERANK_NW4": "1"},
-            "first_pass": {"IMGREC_CHANCE_DIRECT": "0"}}
+            "first_pass": {"IMGREC_CHANCE_DIRECT": "0"}, "direct_raw": {"IMGREC_DIRECT_RAW": "2"}}
 
 
 @pytest.mark.parametrize("nq", [1, 2, 5, 8, 16, 256, 257, 1024])
