@@ -281,6 +281,10 @@ int create_single(int d, int metric, int device, knn_index** out) {
     }
     if (const char* e = test_knob("IMGREC_CHANCE_SKIP")) ix->chance_skip = *e != '0';
     if (const char* e = test_knob("IMGREC_CHANCE_DIRECT")) ix->chance_direct_max = std::max(0, std::atoi(e));
+    if (const char* e = test_knob("IMGREC_I8_HALF_K")) {
+        const int v = std::atoi(e);
+        ix->i8_half_k = v >= 2 ? v : 0;
+    }
     if (const char* e = test_knob("IMGREC_DIRECT_RAW")) ix->direct_raw = std::min(2, std::max(0, std::atoi(e)));
     if (const char* e = test_knob("IMGREC_I8_FUSED_PREP")) ix->i8_fused_prep = *e != '0';
     if (const char* e = test_knob("IMGREC_RERANK_P1")) ix->rerank_p1k = *e != '0';

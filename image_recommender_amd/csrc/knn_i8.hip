@@ -284,7 +284,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
                    int64_t* __restrict__ cand_i, int ncand, const float* __restrict__ qsrc, int d,
                    int dp, int normalize, float* __restrict__ qpad, float* __restrict__ qnorm_out,
                    float* __restrict__ qresid, int* __restrict__ zero_ctl,
-                   float* __restrict__ heads, int raw16) {
+                   float* __restrict__ heads, int raw16, int half_k) {
     // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
     // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
     // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
@@ -322,7 +322,33 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     // for every outstanding load, the prefetch too)
     constexpr int H = (NQ * KM > 64 || NBI > 2) ? 1 : 2;
     constexpr int kSub = 2 / H;                                  // wave steps per 8-row group
-    const int cnt = kSub * (split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0);
+    // Groups round-robin over the splits (group m to split m % nsplit).  half_k = K > 0 (two
+    // workgroups per CU): in every K-th round a second-half split's group goes to its first-half
+    // partner (split - nsplit / 2) — the workgroup dispatched second onto a CU loses issue to the
+    // first and ended ~10 us later (profiles/r05/i8_stamps/, loop_end_by_half)
+    const int h2 = nsplit / 2;
+    const bool first_half = split < h2;
+    const int rs = split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0;    // own rounds
+    int ng = rs;
+    if (half_k > 0) {
+        if (first_half) {
+            const int rp = split + h2 < ngroups ? (ngroups - split - h2 + nsplit - 1) / nsplit : 0;
+            ng = rs + rp / half_k;
+        } else {
+            ng = rs - rs / half_k;
+        }
+    }
+    const int cnt = kSub * ng;
+    // this split's n-th group
+    auto group_of = [&](int n) __attribute__((always_inline)) -> int {
+        if (half_k <= 0) return split + n * nsplit;
+        if (first_half) {
+            const int b = n / (half_k + 1), o = n - b * (half_k + 1);
+            return split + (o == half_k ? h2 : 0) + (b * half_k + min(o, half_k - 1)) * nsplit;
+        }
+        const int b = n / (half_k - 1), o = n - b * (half_k - 1);
+        return split + (b * half_k + o) * nsplit;
+    };
     // One 8-row group per wave step; two register sets, so the next group's loads are in flight
     // while this one's products run (a single set left each wave idle for a whole HBM round trip
     // per group: 4.7 TB/s with three waves per SIMD).
@@ -333,7 +359,7 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         int row[H];
     };
     auto load = [&](int li, Grp& G) __attribute__((always_inline)) {
-        const int m = split + (li / kSub) * nsplit, r0 = m * kGroup + 4 * (li % kSub);
+        const int m = group_of(li / kSub), r0 = m * kGroup + 4 * (li % kSub);
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             G.row[h] = r0 + 4 * h + g;
@@ -712,6 +738,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
         return hipErrorInvalidValue;
     if (!a.qsrc && (!a.qcodes || !a.qscales || !a.qnorm)) return hipErrorInvalidValue;
     if (a.raw16 && (a.nq > 4 || a.ncand < a.nsplit * 16 * a.km)) return hipErrorInvalidValue;
+    if (a.half_k != 0 && (a.half_k < 2 || a.nsplit % 2 != 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);
     const int nbi = (a.nblk + 15) / 16;
 #define IMGREC_I8(NQV, KMV, NBIV)                                                                 \
@@ -719,7 +746,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
                        a.xnorm, a.nrows, a.nblk, a.qcodes, a.qscales, a.qnorm, a.nq, a.nsplit,      \
                        a.id_offset,                                                                 \
                        a.l2, a.cand_d, a.cand_i, a.ncand, a.qsrc, a.d, a.dp, a.normalize, a.qpad,  \
-                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads, a.raw16)
+                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads, a.raw16, a.half_k)
 #define IMGREC_I8_NBI(NQV, KMV)                                   \
     do {                                                          \
         switch (nbi) {                                            \

@@ -109,6 +109,10 @@ struct knn_index {
     // ... over the scan's lane lists unfolded: 1 = while <= 4096 per query, 2 = always, 0 = never
     // (IMGREC_DIRECT_RAW)
     int direct_raw = 1;
+    // int8 scan at two workgroups per CU: every K-th round the second-dispatched half's groups go
+    // to the first half (I8Args::half_k; IMGREC_I8_HALF_K=K, 0 = even split).  12: config 2 one
+    // query 0.1517 -> 0.1503 ms; 6-8 and 24-32 measured worse (profiles/r05/nq1/half_k/)
+    int i8_half_k = 12;
     bool stream_lists = true;   // exact lists of <= 4 queries from one fp32 stream (IMGREC_STREAM_LISTS=0: tiles)
     bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
     bool rerank_nw4 = false;    // IMGREC_RERANK_NW4=1: large batches rerank on 4-wave workgroups

@@ -230,6 +230,9 @@ struct I8Args {
     // <= 4 queries: the split's 16 lane lists written unfolded (16 nsplit lists of km per query;
     // ncand >= 16 nsplit km) and heads = the smallest of their first keys — the direct route
     int raw16 = 0;
+    // > 1: every half_k-th round of row groups, a second-half split's group goes to split -
+    // nsplit / 2 (two workgroups per CU: the one dispatched second gets less work); 0 = even
+    int half_k = 0;
 };
 // Bytes per row of the int8 copy: 64 per block, no padding (round 4; rows were whole 1-KiB
 // groups of 16 blocks, 25 % zeros at d = 768).  Blocks sit in groups of 16 (the scan's 16 lanes of

@@ -353,6 +353,7 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
     a.km = p.km;
     a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
     a.cand_i = ix->cand_i; a.ncand = ncand; a.raw16 = raw ? 1 : 0;
+    if (p.nsplit == 2 * ix->cus) a.half_k = ix->i8_half_k;     // two workgroups per CU
     if (direct) {
         if ((rc = grow(&ix->tail_ctl, &ix->tail_ctl_cap, (size_t)4 + round_up(nq, 32) / 32)) != KNN_OK)
             return rc;

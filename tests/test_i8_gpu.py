@@ -347,3 +347,34 @@ def test_i8_direct_route_exact_rerun_of_crowded_queries(faiss, monkeypatch):
             assert (I == src[:nq, None] * dup + np.arange(10)[None, :]).all(), (raw, nq)
             check_knn(D, I, xb, xq, 10, "l2")
         del idx
+
+
+@pytest.mark.parametrize("d", [100, 768])
+@pytest.mark.parametrize("metric", ["l2", "ip"])
+def test_i8_weighted_halves_match_the_even_split(faiss, monkeypatch, d, metric):
+    """Two scan workgroups per CU (one or two queries): every K-th round of row groups the
+    second-half split's group goes to its first-half partner (I8Args::half_k, round 5).  Every
+    returned bit equals the even split's for K = 2 (a third of the groups moved) and K = 24, over
+    40,003 rows (a ragged last round) and 1-2 queries, search after search."""
+    xb = mixture(40003, d, centres=40, seed=d + 41)
+    xq = mixture(2, d, centres=40, seed=d + 42)
+    idx = {}
+    for name, kk in (("even", "0"), ("k2", "2"), ("k24", "24")):
+        monkeypatch.setenv("IMGREC_I8_HALF_K", kk)
+        idx[name] = _index(faiss, d, metric)          # (the knob is read at index creation)
+        monkeypatch.delenv("IMGREC_I8_HALF_K")
+        idx[name].add(xb)
+        idx[name].search_mode = "i8"
+    for rep in range(2):
+        for nq in (1, 2):
+            q = np.ascontiguousarray(xq[:nq])
+            D0, I0 = idx["even"].search(q, 10)
+            r0 = _stats(idx["even"], nq)
+            for name in ("k2", "k24"):
+                D1, I1 = idx[name].search(q, 10)
+                r1 = _stats(idx[name], nq)
+                if r0 == 0 and r1 == 0:
+                    assert np.array_equal(I1, I0), (name, rep, nq, np.argwhere(I1 != I0)[:5])
+                    assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), (name, rep, nq)
+                if rep == 0:
+                    check_knn(D1, I1, xb, q, 10, metric, min_exact_frac=0.5)
