@@ -124,26 +124,32 @@ i8_rows_kernel(const float* __restrict__ xb, int64_t n, int dp, int nblk, int8_t
 }
 
 // Two-level int8 codes of one 64-element query block, q~ = s_hi c_hi + s_lo c_lo (c_hi =
-// rint(v / s_hi), s_hi = max|v| / 127; c_lo the same of v - s_hi c_hi): emit(lev, e4, word) gets
-// the codes of elements 4 e4 .. 4 e4 + 3 of level lev (0 = hi) as they are made, sc = (s_hi,
-// s_lo); v ends as the residual v - q~; xsq += |v|^2 and rsq += |v - q~|^2.  The one quantiser of
-// i8_query_prep_kernel and the scan's fused prep (bit-identical by construction; the scan writes
-// each word straight to LDS, so no code words are held in registers).
+// rint(v / s_hi), s_hi = max|v| / 127; c_lo the same of v - s_hi c_hi), on 4 lanes: lanes
+// 4g .. 4g + 3 hold one block, quarter q4 = elements 16 q4 .. 16 q4 + 15.  The block maxima meet
+// over the four lanes by shuffles (exact in any order).  emit(lev, e4, word) gets the codes of the
+// block's elements 4 e4 .. 4 e4 + 3 of level lev (0 = hi) as they are made; sc = (s_hi, s_lo); v
+// ends as the residual v - q~; this lane's partial sums xsq += |v|^2, rsq += |v - q~|^2.  The
+// one quantiser of i8_query_prep_kernel and the scan's fused prep (bit-identical by construction:
+// both walk the blocks 16 per pass).  Round 4-5 ran a block on one lane: a 64-element dependent
+// chain, ~3 us of the prep before the scan streams anything.  All four lanes of a group must be
+// active.
 template <class Emit>
-__device__ __forceinline__ void quantize_query_block(float (&v)[kBlk], Emit&& emit, float (&sc)[2],
-                                                     float& xsq, float& rsq) {
+__device__ __forceinline__ void quantize_query_quarter(float (&v)[16], int q4, Emit&& emit,
+                                                       float (&sc)[2], float& xsq, float& rsq) {
     float mx = 0.f;
 #pragma unroll
-    for (int t = 0; t < kBlk; ++t) {
+    for (int t = 0; t < 16; ++t) {
         mx = fmaxf(mx, fabsf(v[t]));
         xsq = fmaf(v[t], v[t], xsq);
     }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
 #pragma unroll
     for (int lev = 0; lev < 2; ++lev) {
         const float sl = mx / 127.f, inv = mx > 0.f ? 127.f / mx : 0.f;
         float mx2 = 0.f;
 #pragma unroll
-        for (int e4 = 0; e4 < kBlk / 4; ++e4) {
+        for (int e4 = 0; e4 < 4; ++e4) {
             uint32_t word = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -152,13 +158,14 @@ __device__ __forceinline__ void quantize_query_block(float (&v)[kBlk], Emit&& em
                 mx2 = fmaxf(mx2, fabsf(v[4 * e4 + t]));
                 word |= ((uint32_t)c & 0xffu) << (8 * t);
             }
-            emit(lev, e4, word);
+            emit(lev, 4 * q4 + e4, word);
         }
         sc[lev] = sl;
-        mx = mx2;
+        mx2 = fmaxf(mx2, __shfl_xor(mx2, 1, 64));
+        mx = fmaxf(mx2, __shfl_xor(mx2, 2, 64));
     }
 #pragma unroll
-    for (int t = 0; t < kBlk; ++t) rsq = fmaf(v[t], v[t], rsq);
+    for (int t = 0; t < 16; ++t) rsq = fmaf(v[t], v[t], rsq);
 }
 
 // |q - q~| bound from the block sums (inflated for its own fp32 evaluation as the rows' is)
@@ -237,20 +244,26 @@ i8_query_prep_kernel(const float* __restrict__ src, int64_t n, int d, int dp, in
     for (int i = dp + lane; i < nblk * kBlk; i += 64) srow[(i >> 6) * kPitch + (i & 63)] = 0.f;
     __syncthreads();
     float rsq = 0.f, xsq = 0.f;
-    if (lane < nblk) {
-        uint32_t w[2][kBlk / 4];
-        float sc[2];
-        float v[kBlk];
+    // four lanes per block, 16 blocks per pass (quantize_query_quarter; the scan's fused prep
+    // walks the blocks the same way, so the sums meet in the same order)
+    for (int b0 = 0; b0 < nblk; b0 += 16) {
+        const int b = b0 + (lane >> 2), q4 = lane & 3;
+        if (b < nblk) {
+            uint32_t w[2][4];
+            float sc[2];
+            float v[16];
 #pragma unroll
-        for (int t = 0; t < kBlk; ++t) v[t] = srow[lane * kPitch + t];
-        quantize_query_block(v, [&](int lev, int e4, uint32_t word) { w[lev][e4] = word; }, sc, xsq, rsq);
-        uint4* out = reinterpret_cast<uint4*>(codes + (row * nblk + lane) * 2 * kBlk);
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-            out[c] = make_uint4(w[c >> 2][4 * (c & 3)], w[c >> 2][4 * (c & 3) + 1],
-                                w[c >> 2][4 * (c & 3) + 2], w[c >> 2][4 * (c & 3) + 3]);
-        scales[(row * nblk + lane) * 2] = sc[0];
-        scales[(row * nblk + lane) * 2 + 1] = sc[1];
+            for (int t = 0; t < 16; ++t) v[t] = srow[b * kPitch + 16 * q4 + t];
+            quantize_query_quarter(v, q4, [&](int lev, int e4, uint32_t word) { w[lev][e4 & 3] = word; },
+                                   sc, xsq, rsq);
+            uint4* out = reinterpret_cast<uint4*>(codes + (row * nblk + b) * 2 * kBlk);
+            out[q4] = make_uint4(w[0][0], w[0][1], w[0][2], w[0][3]);       // words 4 q4 .. + 3
+            out[4 + q4] = make_uint4(w[1][0], w[1][1], w[1][2], w[1][3]);
+            if (q4 == 0) {
+                scales[(row * nblk + b) * 2] = sc[0];
+                scales[(row * nblk + b) * 2 + 1] = sc[1];
+            }
+        }
     }
     rsq = wave_sum(rsq);
     xsq = wave_sum(xsq);
@@ -532,31 +545,36 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) nacc += __shfl_xor(nacc, off, 64);
             float rsq = 0.f, xsq = 0.f;
-            if (lane < nblk) {
-                // lane b's block from the raw row (L1 / L2 after the chunk pass), scaled as the
-                // chunk pass scaled it (the same product); elements past d are zero
-                const int i0 = lane * kBlk;
-                float v[kBlk];
-                if ((d & 3) == 0 && i0 + kBlk <= d) {
+            for (int b0 = 0; b0 < nblk; b0 += 16) {
+                // four lanes per block (quantize_query_quarter): block b's quarter q4 from the raw
+                // row (L1 / L2 after the chunk pass), scaled as the chunk pass scaled it (the same
+                // product); elements past d are zero
+                const int b = b0 + (lane >> 2), q4 = lane & 3;
+                if (b >= nblk) continue;                 // (whole four-lane groups)
+                const int i0 = b * kBlk + 16 * q4;
+                float v[16];
+                if ((d & 3) == 0 && i0 + 16 <= d) {
 #pragma unroll
-                    for (int t4 = 0; t4 < kBlk / 4; ++t4) {
+                    for (int t4 = 0; t4 < 4; ++t4) {
                         const float4 x4 = *reinterpret_cast<const float4*>(s + i0 + 4 * t4);
                         v[4 * t4] = x4.x; v[4 * t4 + 1] = x4.y; v[4 * t4 + 2] = x4.z; v[4 * t4 + 3] = x4.w;
                     }
                 } else {
 #pragma unroll
-                    for (int t = 0; t < kBlk; ++t) v[t] = i0 + t < d ? s[i0 + t] : 0.f;
+                    for (int t = 0; t < 16; ++t) v[t] = i0 + t < d ? s[i0 + t] : 0.f;
                 }
                 if (normalize) {
 #pragma unroll
-                    for (int t = 0; t < kBlk; ++t) v[t] = v[t] * scale;
+                    for (int t = 0; t < 16; ++t) v[t] = v[t] * scale;
                 }
                 float sc[2];
-                uint32_t* qw = reinterpret_cast<uint32_t*>(&sqc[qi][lane][0]);
-                quantize_query_block(v, [&](int lev, int e4, uint32_t word) { qw[lev * (kBlk / 4) + e4] = word; },
-                                     sc, xsq, rsq);
-                sqs[qi][lane][0] = sc[0];
-                sqs[qi][lane][1] = sc[1];
+                uint32_t* qw = reinterpret_cast<uint32_t*>(&sqc[qi][b][0]);
+                quantize_query_quarter(v, q4, [&](int lev, int e4, uint32_t word) { qw[lev * (kBlk / 4) + e4] = word; },
+                                       sc, xsq, rsq);
+                if (q4 == 0) {
+                    sqs[qi][b][0] = sc[0];
+                    sqs[qi][b][1] = sc[1];
+                }
             }
             if (lane == 0) s_qn[qi] = nacc;
             if (split == 0) {
