@@ -104,8 +104,10 @@ struct knn_index {
     bool chance_skip = true;    // IMGREC_CHANCE_SKIP=0: every query takes the first rerank
     // int8 batches of at most this many queries skip the merge and the first rerank: the
     // certificate tail's second chance answers every query (RerankArgs::direct);
-    // IMGREC_CHANCE_DIRECT=N sets it, 0 = off
-    int chance_direct_max = 1;
+    // IMGREC_CHANCE_DIRECT=N sets it, 0 = off.  4: two queries 10 / 5.5 us faster at config 2 / 3,
+    // four queries 9-18 us faster at config 2 and the same at config 3
+    // (profiles/r05/nq1/direct_nq24/)
+    int chance_direct_max = 4;
     // ... over the scan's lane lists unfolded: 1 = while <= 4096 per query, 2 = always, 0 = never
     // (IMGREC_DIRECT_RAW)
     int direct_raw = 1;
