@@ -15,8 +15,11 @@ over RCCL and merged (strong scaling: the corpus is fixed, per-GPU rows shrink a
 `--query-groups 2` runs the query x row partition instead (sharded.py; measured slower per rank at
 N = 2/4/8: profiles/r02/qr_shapes.jsonl).
 
-Contract: `python bench.py --gpus N --steps K --warmup W` (torchrun for N > 1) prints ONE JSON line
-on rank 0.  `value` = Q*K / max-over-ranks wall time of the K steps, inputs resident in HBM.
+Contract: `python bench.py --gpus N --steps K --warmup W` prints ONE JSON line on rank 0.  Under
+torchrun (WORLD_SIZE set) this process is one rank and `--gpus` must equal WORLD_SIZE; started
+plainly with N > 1 it launches the N ranks itself, or exits non-zero when fewer than N GPUs are
+visible (image_recommender_amd/launch.py).  `value` = Q*K / max-over-ranks wall time of the K
+steps, inputs resident in HBM.
 """
 from __future__ import annotations
 
@@ -301,14 +304,16 @@ def pmc_traffic(pattern: str):
 
 def main():
     a = parse()
+    # --gpus N > 1 without torchrun: start the N ranks here (no device touched in this process)
+    # or stop with a non-zero status; never a silent one-GPU run (image_recommender_amd/launch.py)
+    from image_recommender_amd.launch import maybe_spawn
+    maybe_spawn(a.gpus, os.path.abspath(__file__), sys.argv[1:])
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world > 1:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     # IMGREC_DIST_BACKEND=gloo rehearses the N-rank protocol with every rank on one visible GPU
     # (local % device count); the measured runs use RCCL ("nccl"), one rank per GPU
     backend = os.environ.get("IMGREC_DIST_BACKEND", "nccl")

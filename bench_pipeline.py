@@ -206,7 +206,11 @@ def run(a) -> dict | None:
 
 
 def main():
-    out = run(parse())
+    a = parse()
+    # --gpus N > 1 without torchrun: start the N ranks here or stop with a non-zero status
+    from image_recommender_amd.launch import maybe_spawn
+    maybe_spawn(a.gpus, os.path.abspath(__file__), sys.argv[1:])
+    out = run(a)
     if out is not None:
         print(json.dumps(out))
 

@@ -75,3 +75,64 @@ def test_cpu_comparator_single_query_leg():
         D, I = search_blas_fp32_blocked(xb, xq[i:i + 1], 10, block=4096, threads=4, xb_norms=xn)
         Dg, Ig = search_exact(xb, xq[i:i + 1], 10, "l2")
         assert (I == Ig).mean() > 0.9 and np.allclose(D, Dg, rtol=0, atol=1e-5)
+
+
+# ------------------------------------------------------------------------------------------------
+# `--gpus N` launcher (image_recommender_amd/launch.py)
+# ------------------------------------------------------------------------------------------------
+def test_launch_plan_decisions():
+    import pytest
+    from image_recommender_amd.launch import LaunchError, launch_plan
+    never = lambda: (_ for _ in ()).throw(AssertionError("device count not needed"))  # noqa: E731
+    assert launch_plan(1, {}, never) == "single"
+    assert launch_plan(8, {"WORLD_SIZE": "8"}, never) == "rank"          # torchrun started us
+    assert launch_plan(2, {}, 8) == "spawn"
+    assert launch_plan(8, {}, lambda: 8) == "spawn"
+    with pytest.raises(LaunchError, match="sees 1"):                      # one-GPU box, RCCL
+        launch_plan(8, {}, 1)
+    with pytest.raises(LaunchError, match="WORLD_SIZE=2"):                # mismatched torchrun
+        launch_plan(8, {"WORLD_SIZE": "2"}, 8)
+    with pytest.raises(LaunchError):
+        launch_plan(0, {}, 8)
+    # the gloo rehearsal shares the visible device(s): one is enough, none is not
+    assert launch_plan(2, {"IMGREC_DIST_BACKEND": "gloo"}, 1) == "spawn"
+    with pytest.raises(LaunchError, match="no visible GPU"):
+        launch_plan(2, {"IMGREC_DIST_BACKEND": "gloo"}, 0)
+    assert launch_plan(2, {"IMGREC_DIST_BACKEND": "gloo"}, 0, require_gpu=False) == "spawn"
+
+
+def _probe(args, **env):
+    import subprocess
+    import sys
+    from pathlib import Path
+    probe = Path(__file__).with_name("launch_probe.py")
+    e = dict(__import__("os").environ)
+    for key in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(key, None)
+    e.update(env)
+    return subprocess.run([sys.executable, str(probe)] + args, env=e, capture_output=True,
+                          text=True, timeout=120)
+
+
+def test_launcher_starts_n_ranks_without_torchrun():
+    """`script --gpus 3` (no torchrun) runs 3 ranks: rank 0's line reports world_size 3 and the
+    all-reduce of 1 + 2 + 3."""
+    r = _probe(["3"], IMGREC_DIST_BACKEND="gloo")
+    assert r.returncode == 0, r.stderr
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert lines == [{"world_size": 3, "sum": 6.0}], r.stdout
+
+
+def test_launcher_fails_without_enough_gpus():
+    """RCCL needs one GPU per rank: with 1 visible the run exits non-zero before any work."""
+    r = _probe(["2"], IMGREC_DIST_BACKEND="nccl", PROBE_VISIBLE="1")
+    assert r.returncode == 2 and "needs 2 visible GPUs" in r.stderr, (r.returncode, r.stderr)
+    assert r.stdout == ""
+
+
+def test_launcher_reports_a_failing_rank():
+    """A rank that exits 3 ends the run with status 3, and the rank blocked in the collective is
+    stopped instead of hanging."""
+    r = _probe(["2", "1"], IMGREC_DIST_BACKEND="gloo")
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "rank 1 exited with status 3" in r.stderr
