@@ -64,7 +64,8 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--query-groups", type=int, default=1,
                     help="query slices of the N ranks (sharded.py query x row partition)")
-    ap.add_argument("--gt-queries", type=int, default=128, help="queries checked for recall@k")
+    ap.add_argument("--gt-queries", type=int, default=1024,
+                    help="queries checked for recall@k (default: the whole batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--single-query-steps", type=int, default=50)
@@ -460,6 +461,7 @@ def main():
     got_d = Dr[:ngt].cpu().numpy()
     hits = sum(len(set(x.tolist()) & set(y.tolist())) for x, y in zip(got_i, gt_i))
     recall = hits / (a.k * ngt)
+    label_eq = float((got_i == gt_i).mean())       # rank-by-rank equality with float64's labels
     max_dist_err = float(np.max(np.abs(got_d.astype(np.float64) - gt_d)))
 
     # single-query latency regime (the CLI's nq = 1 path; HBM-bound)
@@ -538,6 +540,7 @@ def main():
             },
             "recall_at_10": recall,
             "recall_queries": ngt,
+            "labels_equal_fp64_frac": label_eq,
             "max_abs_dist_err_vs_fp64": max_dist_err,
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": peak,
