@@ -12,7 +12,8 @@ Now the entry process decides first, before torch touches a device:
   the same script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR = 127.0.0.1 / MASTER_PORT set,
   the environment torchrun gives its workers.  The parent never initialises a device and never
   replaces itself (no exec): it waits, stops the other ranks as soon as one fails, and exits with
-  the worst child status.  Rank 0's JSON line goes straight to the inherited stdout.
+  the first failing rank's status.  Only rank 0's JSON lines reach stdout; every other line any
+  rank writes to stdout (gloo's connection banners, say) is passed to stderr.
 * Too few devices for one rank per GPU over RCCL: exit non-zero before any work.  With
   IMGREC_DIST_BACKEND=gloo (a rehearsal of the N-rank protocol on one box) every rank shares the
   visible device(s), so one device is enough.
@@ -28,6 +29,7 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 
@@ -102,11 +104,21 @@ def spawn(script: str, argv, world: int, env=None, poll_s: float = 0.2,
     waiting in a collective for a dead peer does not hang the run."""
     base = dict(os.environ if env is None else env)
     port = free_port()
-    procs = []
+    procs, pumps = [], []
+
+    def pump(stream, rank):
+        for line in iter(stream.readline, ""):
+            out = sys.stdout if rank == 0 and line.lstrip().startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
+        stream.close()
     try:
         for r in range(world):
             procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv),
-                                          env=rank_env(base, r, world, port)))
+                                          env=rank_env(base, r, world, port),
+                                          stdout=subprocess.PIPE, text=True, bufsize=1))
+            pumps.append(threading.Thread(target=pump, args=(procs[-1].stdout, r), daemon=True))
+            pumps[-1].start()
         worst, failed_at = 0, None
         while True:
             alive = 0
@@ -124,6 +136,8 @@ def spawn(script: str, argv, world: int, env=None, poll_s: float = 0.2,
                             if q.poll() is None:
                                 q.send_signal(signal.SIGTERM)
             if alive == 0:
+                for t in pumps:
+                    t.join(timeout=5.0)
                 return worst
             if failed_at is not None and time.monotonic() - failed_at > grace_s:
                 for q in procs:

@@ -3,8 +3,9 @@
 The host oracle (oracle.flat_knn.search_exact, numpy float64) takes ~1 s per query at 1M x 1968,
 so the full-size tests used to check a sample of 16-32 of the 1024 queries.  This scan checks
 every query in seconds: the corpus is streamed block by block (device tensors in global row
-order), each block's float64 keys (|q|^2 + |x|^2 - 2 q.x in float64 GEMMs on the device) are
-folded into a running top-k in (key, label) order — exact ties by the smaller label, faiss
+order), each block's float64 squared-L2 keys (|q|^2 + |x|^2 - 2 q.x in float64 GEMMs on the device
+select a block's best; those are recomputed as sum((x - q)^2) in float64, so exact duplicates tie
+exactly) are folded into a running top-k in (key, label) order — exact ties by the smaller label, faiss
 IndexFlat's order — and, beside it, the top-(k-1) by faiss IndexFlatL2's own fp32 key form (fp32
 GEMM per block, clamped at 0: exhaustive_L2sqr_blas restated, the `blas` input of
 tests/knn_check.check_knn_tight).
@@ -57,10 +58,13 @@ def device_topk(torch, blocks, qs, k: int, row0: int = 0, need=None, collect_row
         dd = (qn + (xd * xd).sum(1)[None, :] - 2.0 * (qd @ xd.T)).clamp_min_(0.0)
         # a block's k smallest keys, ties at the k-th included (topk may pick any of equal keys)
         v, i = torch.topk(dd, min(k, n), dim=1, largest=False)
-        tie = (dd <= v[:, -1:]).sum(1).max().item()
+        tie = (dd <= v[:, -1:] + 1e-12 * (1.0 + v[:, -1:].abs())).sum(1).max().item()
         if tie > v.shape[1]:
             v, i = torch.topk(dd, min(int(tie), n), dim=1, largest=False)
         del dd, xd
+        # the selected keys again in the difference form sum((x - q)^2) (float64): the expanded
+        # form leaves ~1e-16 noise on exact duplicates, which would order tied copies at random
+        v = torch.stack([((blk[i[:, j]].double() - qd) ** 2).sum(1) for j in range(i.shape[1])], 1)
         cd = torch.cat([bd, v], 1)
         ci = torch.cat([bi, i + pos], 1)
         # (key, label) order: a stable sort by label, then a stable sort by key

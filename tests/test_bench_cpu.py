@@ -119,7 +119,8 @@ def test_launcher_starts_n_ranks_without_torchrun():
     all-reduce of 1 + 2 + 3."""
     r = _probe(["3"], IMGREC_DIST_BACKEND="gloo")
     assert r.returncode == 0, r.stderr
-    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    # stdout carries rank 0's JSON line only (gloo's banners and other ranks' output: stderr)
+    lines = [json.loads(x) for x in r.stdout.splitlines()]
     assert lines == [{"world_size": 3, "sum": 6.0}], r.stdout
 
 

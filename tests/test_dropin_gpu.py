@@ -64,11 +64,20 @@ def test_search_matches_reference(built):
         assert len(got) == len(want)
         gd = np.array([d for _, d in got])
         wd = np.array([d for _, d in want])
-        np.testing.assert_allclose(gd, wd, rtol=0, atol=2e-5)
-        # identical ranking up to exact/near ties (equal distances may swap)
-        for (gp, g_d), (wp, w_d) in zip(got, want):
-            if gp != wp:
-                assert any(abs(w_d - d2) <= 2e-5 and p2 == gp for p2, d2 in want), (gp, wp)
+        # the empirical window of tests/knn_check.check_knn_tight: 8 x this build's measured
+        # |fp32 - float64| distance error, at least 1e-6 of the key scale, with that error first
+        # held below 32 unit roundoffs of the key's term scale (|q|^2 + |x|^2 <= 1 + 3: the query
+        # is normalised, a stored row has at most three unit-norm parts)
+        err = float(np.abs(gd - wd).max())
+        assert err <= 32 * 2.0 ** -24 * 4.0, (s["paths"], err)
+        w = max(8.0 * err, 1e-6 * float(np.abs(wd).max()))
+        for j, ((gp, g_d), (wp, w_d)) in enumerate(zip(got, want)):
+            lo = j == 0 or abs(wd[j] - wd[j - 1]) > w
+            hi = j + 1 >= len(wd) or abs(wd[j + 1] - wd[j]) > w
+            if lo and hi:
+                assert gp == wp, (s["paths"], j, got, want, w)      # integer-exact label
+            else:            # inside a tie window: the label is one of the window's labels
+                assert any(abs(w_d - d2) <= w and p2 == gp for p2, d2 in want), (gp, wp, w)
 
 
 def test_index_resident_across_searches(built):
