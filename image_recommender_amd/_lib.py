@@ -17,7 +17,7 @@ LIB_PATH = Path(__file__).resolve().parent / "lib" / os.environ.get("IMGREC_LIB_
 KNN_OK, KNN_EINVAL, KNN_EHIP, KNN_ENOMEM, KNN_EIO, KNN_ENOSYS = 0, -1, -2, -3, -4, -5
 KNN_METRIC_IP, KNN_METRIC_L2, KNN_METRIC_COSINE = 0, 1, 2
 KNN_MAX_K = 32          # fused top-k kernels (include/imgrec_knn.h)
-KNN_MAX_K_LARGE = 1024  # largest k of a search (GEMM + select beyond KNN_MAX_K)
+KNN_MAX_K_LARGE = 1024  # largest k of the in-LDS large-k route; beyond it the sort route (any k)
 KNN_SEARCH_AUTO, KNN_SEARCH_EXACT, KNN_SEARCH_SPLIT, KNN_SEARCH_BF16, KNN_SEARCH_I8 = 0, 1, 2, 3, 4
 KNN_FENCE_EAGER, KNN_FENCE_LAZY = 0, 1
 COLOR_HIST_MAX_BINS = 32

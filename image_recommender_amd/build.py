@@ -31,7 +31,7 @@ ARCH = os.environ.get("IMGREC_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["knn_kernels.hip", "knn_b16.hip", "knn_b16w.hip", "knn_refine.hip", "knn_capi.cpp", "knn_plan.cpp",
            "knn_search.cpp", "knn_multi.cpp", "knn_io.cpp", "ivfpq_capi.cpp", "color_hist.hip",
-           "ingest.cpp", "ivfpq.hip", "knn_largek.hip", "vit_fused.hip", "vit_attn.hip", "knn_i8.hip", "vit_gemm.hip"]
+           "ingest.cpp", "ivfpq.hip", "knn_largek.hip", "knn_hugek.hip", "vit_fused.hip", "vit_attn.hip", "knn_i8.hip", "vit_gemm.hip"]
 HEADERS = ["knn_kernels.h", "knn_index.h", "knn_multi.h", "wave_ops.h", "knn_certify.h", "lds_dma.h", "../../include/imgrec_ivfpq.h",
            "../../include/imgrec_knn.h", "../../include/imgrec_color.h", "../../include/imgrec_ingest.h",
            "../../include/imgrec_vit.h"]

@@ -73,6 +73,17 @@ static_assert(kBKW == 32 && kCPR == 8, "stage depth: two 32-deep k-steps per sta
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
 static_assert(kDeferQ >= 0 && kDeferQ < kQuads - 1, "deferred DMA inside the stage's first quads");
+// Screen early-out (A/B): per row group first the lane minimum of the screen values, two rows per
+// v_pk_min, and the per-row sign masks only when some lane of the wave has a passing row (the
+// full test is a superset check: rows at exactly the threshold take the full path)
+#ifndef IMGREC_B16W_SCREEN_MIN
+#define IMGREC_B16W_SCREEN_MIN 0
+#endif
+// Measurement builds only (tools/b16w_epi_split.sh; the lists they return are wrong):
+// 1 = no per-tile epilogue (the stage loop alone), 2 = the screen without the insertions
+#ifndef IMGREC_B16W_EPI_EXP
+#define IMGREC_B16W_EPI_EXP 0
+#endif
 
 // Ascending register list, labels arriving in increasing order per lane: slot p's key is the
 // median of (kd[p-1], d, kd[p]); selects stay v_cndmask (no branches); d = +inf is a no-op.
@@ -430,10 +441,32 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
         };
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
-            if (rg >= nlive) break;
+            if (rg >= nlive || IMGREC_B16W_EPI_EXP == 1) break;
             // row group rg = row blocks 4 rg .. 4 rg + 3; bit 4 j + i of a mask = accumulator
             // register i of row block 4 rg + j = tile row (4 rg + j) * 16 + 4 lq + i
             screen();
+#if IMGREC_B16W_SCREEN_MIN
+            {
+                f32x2 mn[2] = {(f32x2){INFINITY, INFINITY}, (f32x2){INFINITY, INFINITY}};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int rb = 4 * rg + j;
+                    float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (L2) n4 = *reinterpret_cast<const float4*>(nrm + rb * 16 + 4 * lq);
+                    const f32x2 half2 = (f32x2){0.5f - kLo, 0.5f - kLo};
+                    const f32x2 hlo = (f32x2){n4.x, n4.y} * half2, hhi = (f32x2){n4.z, n4.w} * half2;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const f32x2 c2 = (f32x2){cth[h], cth[h]};
+                        const f32x2 dhi = (L2 ? hhi + c2 : c2) - (f32x2){acc[rb][h][2], acc[rb][h][3]};
+                        const f32x2 dlo = (L2 ? hlo + c2 : c2) - (f32x2){acc[rb][h][0], acc[rb][h][1]};
+                        mn[h] = __builtin_elementwise_min(mn[h], __builtin_elementwise_min(dhi, dlo));
+                    }
+                }
+                const f32x2 m2 = __builtin_elementwise_min(mn[0], mn[1]);
+                if (!__any(fminf(m2.x, m2.y) <= 0.f)) continue;    // no row of the group passes
+            }
+#endif
             unsigned live = 0xffffu;
             if (!full) {
                 live = 0;
@@ -461,6 +494,12 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
             }
 #ifdef IMGREC_B16_STAMPS
             const unsigned long long ins0 = __builtin_amdgcn_s_memtime();
+#endif
+#if IMGREC_B16W_EPI_EXP == 2
+            // (keep the screen live: fold its masks into list entry 0, never an insertion)
+            kp[0][0] ^= (msk[0] & live) & 0x80000000u;
+            kp[1][0] ^= (msk[1] & live) & 0x80000000u;
+            continue;
 #endif
 #pragma unroll
             for (int h = 0; h < 2; ++h) {

@@ -322,6 +322,7 @@ void free_single(knn_index* ix) {
                     (void*)ix->fb_q, (void*)ix->fb_qn, (void*)ix->hq, (void*)ix->hd, (void*)ix->hi})
         if (p) (void)hipFree(p);
     largek_free(ix);
+    hugek_free(ix);
     for (hipEvent_t e : ix->ev) (void)hipEventDestroy(e);
     if (ix->fence) (void)hipEventDestroy(ix->fence);
     (void)hipStreamDestroy(ix->stream);
@@ -464,8 +465,7 @@ int knn_reconstruct_n(const knn_index_t* cix, int64_t i0, int64_t n, float* x) {
 int knn_search_device(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                       void* stream) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (k <= 0 || k > KNN_MAX_K_LARGE)
-        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
+    if (k <= 0) KNN_FAIL(KNN_EINVAL, "k must be >= 1 (got %d)", k);
     if (nq < 0 || (nq > 0 && (!q || !D || !I))) KNN_FAIL(KNN_EINVAL, "bad query/output pointers");
     if (nq == 0) return KNN_OK;
     if (ix->multi) return multi_search_device(ix, q, nq, k, D, I, (hipStream_t)stream);
@@ -497,8 +497,7 @@ constexpr size_t kPinnedSearchBytes = 1 << 20;
 
 int knn_search(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int64_t* I) {
     if (!ix) KNN_FAIL(KNN_EINVAL, "index is NULL");
-    if (k <= 0 || k > KNN_MAX_K_LARGE)
-        KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
+    if (k <= 0) KNN_FAIL(KNN_EINVAL, "k must be >= 1 (got %d)", k);
     if (nq < 0 || (nq > 0 && (!q || !D || !I))) KNN_FAIL(KNN_EINVAL, "bad query/output pointers");
     if (nq == 0) return KNN_OK;
     if (ix->multi) return multi_search(ix, q, nq, k, D, I);
@@ -536,15 +535,13 @@ int knn_search(knn_index_t* ix, const float* q, int64_t nq, int k, float* D, int
 int knn_merge_device(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin, int k,
                      int metric, float* D, int64_t* I, void* stream) {
     if (nlists <= 0 || kin <= 0 || nq < 0) KNN_FAIL(KNN_EINVAL, "bad merge shape");
-    if (k <= 0 || k > KNN_MAX_K_LARGE) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
-    if (k > KNN_MAX_K && (int64_t)nlists * kin > 8192)
-        KNN_FAIL(KNN_EINVAL, "k > %d merges at most 8192 entries per query (%d x %d)", KNN_MAX_K, nlists, kin);
+    if (k <= 0) KNN_FAIL(KNN_EINVAL, "k must be >= 1 (got %d)", k);
     if (nq == 0) return KNN_OK;
     if (!cD || !cI || !D || !I) KNN_FAIL(KNN_EINVAL, "NULL pointer");
     const int kmetric = metric == KNN_METRIC_L2 ? 1 : 0;
     if (k > KNN_MAX_K) {
-        KNN_HIP(launch_merge_large(cD, cI, nlists, nq, kin, nq * (int64_t)kin, nq * (int64_t)kin, k,
-                                   kmetric, D, I, (hipStream_t)stream));
+        KNN_HIP(launch_merge_any(cD, cI, nlists, nq, kin, nq * (int64_t)kin, nq * (int64_t)kin, k,
+                                 kmetric, D, I, (hipStream_t)stream));
         return KNN_OK;
     }
     KNN_HIP(launch_merge(cD, cI, nq, nlists, kin, kin, nq * (int64_t)kin, k, kmetric,
@@ -561,9 +558,7 @@ int64_t knn_packed_bytes(int64_t nq, int k) {
 int knn_merge_packed_device(const void* packed, int nlists, int64_t nq, int kin, int k, int metric,
                             float* D, int64_t* I, void* stream) {
     if (nlists <= 0 || kin <= 0 || nq < 0) KNN_FAIL(KNN_EINVAL, "bad merge shape");
-    if (k <= 0 || k > KNN_MAX_K_LARGE) KNN_FAIL(KNN_EINVAL, "k must be in [1, %d] (got %d)", KNN_MAX_K_LARGE, k);
-    if (k > KNN_MAX_K && (int64_t)nlists * kin > 8192)
-        KNN_FAIL(KNN_EINVAL, "k > %d merges at most 8192 entries per query (%d x %d)", KNN_MAX_K, nlists, kin);
+    if (k <= 0) KNN_FAIL(KNN_EINVAL, "k must be >= 1 (got %d)", k);
     if (nq == 0) return KNN_OK;
     if (!packed || !D || !I) KNN_FAIL(KNN_EINVAL, "NULL pointer");
     const int64_t n = nq * kin, nf = n + (n & 1);
@@ -571,8 +566,8 @@ int knn_merge_packed_device(const void* packed, int nlists, int64_t nq, int kin,
     const int64_t* cI = reinterpret_cast<const int64_t*>(static_cast<const char*>(packed) + nf * 4);
     const int kmetric = metric == KNN_METRIC_L2 ? 1 : 0;
     if (k > KNN_MAX_K) {
-        KNN_HIP(launch_merge_large(cD, cI, nlists, nq, kin, nf + 2 * n, nf / 2 + n, k, kmetric, D, I,
-                                   (hipStream_t)stream));
+        KNN_HIP(launch_merge_any(cD, cI, nlists, nq, kin, nf + 2 * n, nf / 2 + n, k, kmetric, D, I,
+                                 (hipStream_t)stream));
         return KNN_OK;
     }
     // chunk = nf floats + n int64: nf + 2n floats, nf / 2 + n int64
@@ -661,14 +656,27 @@ int knn_last_path(const knn_index_t* ix) {
     return ix->multi ? multi_last_path(ix) : ix->last_path;
 }
 
-int knn_large_k_fallbacks(const knn_index_t* ix, int64_t* n) {
-    if (!ix || !n) KNN_FAIL(KNN_EINVAL, "NULL argument");
-    if (!ix->multi) {
-        *n = ix->lk_last_fallbacks;
-        return KNN_OK;
-    }
+// The count lives on the device (the large-k search never waits for the GPU): reading it waits
+// for the index's last operation.
+static int large_k_fallbacks_one(knn_index* ix, int64_t* n) {
+    std::lock_guard<std::mutex> lk(ix->mu);
+    DeviceGuard g(ix->device);
+    const int rc = largek_fallbacks(ix, n);
+    if (rc != KNN_OK) return rc;
+    return fence_end_synced(ix);
+}
+
+int knn_large_k_fallbacks(const knn_index_t* cix, int64_t* n) {
+    if (!cix || !n) KNN_FAIL(KNN_EINVAL, "NULL argument");
+    knn_index* ix = const_cast<knn_index*>(cix);     // (only the fence state changes)
+    if (!ix->multi) return large_k_fallbacks_one(ix, n);
     *n = 0;
-    for (int s = 0; s < multi_num_shards(ix); ++s) *n += multi_shard(ix, s)->lk_last_fallbacks;
+    for (int s = 0; s < multi_num_shards(ix); ++s) {
+        int64_t v = 0;
+        const int rc = large_k_fallbacks_one(const_cast<knn_index*>(multi_shard(ix, s)), &v);
+        if (rc != KNN_OK) return rc;
+        *n += v;
+    }
     return KNN_OK;
 }
 

@@ -755,6 +755,8 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
                    !a.qnorm_out || !a.qresid))
         return hipErrorInvalidValue;
     if (!a.qsrc && (!a.qcodes || !a.qscales || !a.qnorm)) return hipErrorInvalidValue;
+    // the in-scan query prep serves at most 4 queries: the 5-8 query instance reads qcodes
+    if (a.qsrc && a.nq > 4) return hipErrorInvalidValue;
     if (a.raw16 && (a.nq > 4 || a.ncand < a.nsplit * 16 * a.km)) return hipErrorInvalidValue;
     if (a.half_k != 0 && (a.half_k < 2 || a.nsplit % 2 != 0)) return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);

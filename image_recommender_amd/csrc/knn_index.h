@@ -204,8 +204,14 @@ struct knn_index {
     struct knn_multi* multi = nullptr;
     // k > KNN_MAX_K (knn_largek.hip): the fallback's stripe lists, the uncertified queries (+ count)
     uint64_t* lk_run = nullptr; size_t lk_run_cap = 0;
+    // a chunk's failed queries, then their count and the last large-k search's total (device)
     int* lk_fail = nullptr; size_t lk_fail_cap = 0;
-    int64_t lk_last_fallbacks = 0;   // queries the large-k certificate sent to the exact scan (total)
+    // k > KNN_MAX_K_LARGE (knn_hugek.hip): a query chunk's keys, sorted keys, segment offsets, and
+    // the sort's temporary storage (bytes)
+    uint64_t* hk_a = nullptr; size_t hk_a_cap = 0;
+    uint64_t* hk_b = nullptr; size_t hk_b_cap = 0;
+    unsigned* hk_off = nullptr; size_t hk_off_cap = 0;
+    void* hk_tmp = nullptr; size_t hk_tmp_cap = 0;
 };
 
 namespace imgrec {
@@ -241,10 +247,24 @@ int stream_splits(const knn_index* ix);
 hipError_t launch_stream_lists(const knn_index* ix, const float* qpad, const float* qnorm, int64_t nq,
                                int metric, int sp, float* cd, int64_t* ci, hipStream_t st);
 void largek_free(knn_index* ix);
+// queries the last large-k search sent to the exact scan (a device count; waits for the index)
+int largek_fallbacks(knn_index* ix, int64_t* n);
 // merge of nlists sorted per-shard lists for KNN_MAX_K < k (nlists * kin <= 8192; labels < 2^32)
 hipError_t launch_merge_large(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin,
                               int64_t sd, int64_t si, int k, int metric, float* D, int64_t* I,
                               hipStream_t st);
 bool use_split(const knn_index* ix, int64_t nq, int k);
+// knn_hugek.hip: k > KNN_MAX_K_LARGE — every (query, row) key, a segmented sort per query
+int hugek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
+                 hipStream_t st);
+void hugek_free(knn_index* ix);
+// merge of nlists sorted lists of kin entries per query for any k (labels < 2^32)
+hipError_t launch_merge_huge(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin,
+                             int64_t sd, int64_t si, int k, int metric, float* D, int64_t* I,
+                             hipStream_t st);
+// the large-k list merge when it fits the in-LDS select (nlists * kin <= 8192), else the sort
+hipError_t launch_merge_any(const float* cD, const int64_t* cI, int nlists, int64_t nq, int kin,
+                            int64_t sd, int64_t si, int k, int metric, float* D, int64_t* I,
+                            hipStream_t st);
 
 }  // namespace imgrec

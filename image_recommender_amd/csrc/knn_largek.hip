@@ -14,10 +14,12 @@
 //      corpus's.  With rows interleaved over the splits in 8-row groups a list holds ~k / lists of
 //      the answer (4 at k = 1024 over 256 lists), so the certificate fails only when one list's
 //      rows crowd the answer (or k approaches the corpus size);
-//   3. the queries it leaves (counted on the device, read back by the host: the one place this
-//      path waits for the GPU) are re-run by an exact scan: S stripes of the corpus per query,
-//      each a workgroup computing its rows' fp32 keys (one wave per row) into LDS and folding
-//      them into a running top-k with the same select, then the S lists merged.
+//   3. the queries it leaves (listed and counted on the device) are re-run by an exact scan: S
+//      stripes of the corpus per query, each a workgroup computing its rows' fp32 keys (one wave
+//      per row) into LDS and folding them into a running top-k with the same select, then the S
+//      lists merged.  The scan's grid is fixed (S stripes x kLKFailWG workgroups that walk the
+//      failed queries the device counted), so the host never waits: with every query certified
+//      the scan's workgroups read the count and exit (a few us).
 // Radix select (select_k): the values are u64 (order-preserving key bits | local row: unsigned
 // order = (key, row), faiss's tie rule); eight 8-bit digit passes of a 256-bin LDS histogram find
 // the k-th smallest T; the values < T, then copies of T, fill the result (empties = ~0 pad a
@@ -38,6 +40,9 @@ namespace {
 
 constexpr int kLKThreads = 256;
 constexpr int kLKM = 8192;          // LDS values per query: running list + corpus block
+constexpr int64_t kLKChunk = 1024;  // queries per chunk: bounds the scan's stripe lists (run) to
+                                    // kLKChunk x 8192 u64 = 64 MiB
+constexpr int kLKFailWG = 64;       // scan / final workgroups walking a chunk's failed queries
 constexpr int kLKSort = 1024;       // KNN_MAX_K_LARGE, a power of two
 static_assert(KNN_MAX_K_LARGE <= kLKSort && (kLKSort & (kLKSort - 1)) == 0, "sort width");
 
@@ -275,7 +280,7 @@ __global__ void __launch_bounds__(kLKThreads)
 largek_union_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci, int nlists, int km,
                     int ncand, int k, int64_t ntotal, int metric, int64_t id_offset,
                     float* __restrict__ D, int64_t* __restrict__ I, int* __restrict__ fail_list,
-                    int* __restrict__ fail_cnt) {
+                    int* __restrict__ fail_cnt, int* __restrict__ fail_total) {
     __shared__ uint64_t v[kLKM];
     __shared__ uint64_t sel[kLKSort];
     __shared__ uint32_t hist[256];
@@ -312,26 +317,22 @@ largek_union_kernel(const float* __restrict__ cd, const int64_t* __restrict__ ci
         write_topk(sel, k, metric, id_offset, D + q * k, I + q * k);
     } else if (t == 0) {
         fail_list[atomicAdd(fail_cnt, 1)] = (int)q;
+        atomicAdd(fail_total, 1);
     }
 }
 
-// Step 3, a workgroup per (stripe s = blockIdx.x, failing query f = blockIdx.y): the exact fp32
-// keys of rows [s R, (s + 1) R) — one wave per row, lanes over the row's float4s, a shuffle
-// reduction — folded chunk by chunk into a running top-k (select_k), written to
-// run[(f S + s) k ...].  qpad / qnorm: the query block's padded rows and norms.
-__global__ void __launch_bounds__(kLKThreads)
-largek_scan_kernel(const float* __restrict__ xb, const float* __restrict__ xn, int64_t ntotal, int dp,
-                   const float* __restrict__ qpad, const float* __restrict__ qnorm,
-                   const int* __restrict__ fail_list, int f0, int64_t R, int k, int metric,
-                   uint64_t* __restrict__ run) {
+// One (stripe, failed query) item of largek_scan_kernel (workgroup-uniform arguments).
+__device__ void largek_scan_one(const float* __restrict__ xb, const float* __restrict__ xn, int64_t ntotal,
+                                int dp, const float* __restrict__ qpad, const float* __restrict__ qnorm,
+                                int q, int f, int64_t R, int k, int metric, uint64_t* __restrict__ run) {
     __shared__ uint64_t v[kLKM];
     __shared__ uint64_t sel[kLKSort];
     __shared__ uint32_t hist[256];
     __shared__ uint64_t s_prefix;
     __shared__ int s_rem, s_nlt;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int S = gridDim.x, s = blockIdx.x, f = blockIdx.y;
-    const int q = fail_list[f0 + f];
+    const int S = gridDim.x, s = blockIdx.x;
+    __syncthreads();                                    // the previous item's LDS reads are done
     const float4* q4 = reinterpret_cast<const float4*>(qpad + (int64_t)q * dp);
     const float qn = qnorm[q];
     const int64_t r0 = (int64_t)s * R, r1 = min(ntotal, r0 + R);
@@ -369,22 +370,43 @@ largek_scan_kernel(const float* __restrict__ xb, const float* __restrict__ xn, i
     for (int i = t; i < k; i += kLKThreads) out[i] = sel[i];
 }
 
-// The S stripe lists of failing query f (S * k <= kLKM) -> its final sorted top-k in D / I.
+// Step 3, a workgroup per (stripe s = blockIdx.x, failed queries f = blockIdx.y, + gridDim.y, ...
+// below the device's count): the exact fp32 keys of rows [s R, (s + 1) R) — one wave per row,
+// lanes over the row's float4s, a shuffle reduction — folded chunk by chunk into a running top-k
+// (select_k), written to run[(f S + s) k ...].  qpad / qnorm: the query block's padded rows and
+// norms.
+__global__ void __launch_bounds__(kLKThreads)
+largek_scan_kernel(const float* __restrict__ xb, const float* __restrict__ xn, int64_t ntotal, int dp,
+                   const float* __restrict__ qpad, const float* __restrict__ qnorm,
+                   const int* __restrict__ fail_list, const int* __restrict__ fail_cnt, int64_t R,
+                   int k, int metric, uint64_t* __restrict__ run) {
+    const int nfail = *fail_cnt;                        // written by largek_union_kernel
+    for (int f = blockIdx.y; f < nfail; f += gridDim.y)
+        largek_scan_one(xb, xn, ntotal, dp, qpad, qnorm, fail_list[f], f, R, k, metric, run);
+}
+
+// The S stripe lists of each failed query f (S * k <= kLKM; f = blockIdx.x, + gridDim.x, ...
+// below the device's count) -> its final sorted top-k in D / I.
 __global__ void __launch_bounds__(kLKThreads)
 largek_final_kernel(const uint64_t* __restrict__ run, int S, int k, const int* __restrict__ fail_list,
-                    int f0, int metric, int64_t id_offset, float* __restrict__ D, int64_t* __restrict__ I) {
+                    const int* __restrict__ fail_cnt, int metric, int64_t id_offset,
+                    float* __restrict__ D, int64_t* __restrict__ I) {
     __shared__ uint64_t v[kLKM];
     __shared__ uint64_t sel[kLKSort];
     __shared__ uint32_t hist[256];
     __shared__ uint64_t s_prefix;
     __shared__ int s_rem, s_nlt;
-    const int t = threadIdx.x, f = blockIdx.x;
-    const int q = fail_list[f0 + f];
+    const int t = threadIdx.x;
+    const int nfail = *fail_cnt;
     const int M = S * k;
-    for (int e = t; e < M; e += kLKThreads) v[e] = run[(int64_t)f * M + e];
-    __syncthreads();
-    select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, true);
-    write_topk(sel, k, metric, id_offset, D + (int64_t)q * k, I + (int64_t)q * k);
+    for (int f = blockIdx.x; f < nfail; f += gridDim.x) {
+        const int q = fail_list[f];
+        __syncthreads();                                // the previous query's LDS reads are done
+        for (int e = t; e < M; e += kLKThreads) v[e] = run[(int64_t)f * M + e];
+        __syncthreads();
+        select_k(v, M, k, sel, hist, &s_prefix, &s_rem, &s_nlt, true);
+        write_topk(sel, k, metric, id_offset, D + (int64_t)q * k, I + (int64_t)q * k);
+    }
 }
 
 // Merge of nlists sorted per-shard results of kin entries per query (distance-ascending for L2,
@@ -462,6 +484,18 @@ hipError_t launch_stream_lists(const knn_index* ix, const float* qpad, const flo
     return hipGetLastError();
 }
 
+int largek_fallbacks(knn_index* ix, int64_t* n) {
+    *n = 0;
+    if (!ix->lk_fail) return KNN_OK;
+    int rc;
+    if ((rc = fence_begin(ix, ix->stream)) != KNN_OK) return rc;
+    int v = 0;
+    KNN_HIP(hipMemcpyAsync(&v, ix->lk_fail + kLKChunk + 1, sizeof(int), hipMemcpyDeviceToHost, ix->stream));
+    KNN_HIP(hipStreamSynchronize(ix->stream));
+    *n = v;
+    return KNN_OK;
+}
+
 void largek_free(knn_index* ix) {
     for (void* p : {(void*)ix->lk_run, (void*)ix->lk_fail})
         if (p) (void)hipFree(p);
@@ -479,15 +513,18 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         return KNN_OK;
     }
     int rc;
-    ix->lk_last_fallbacks = 0;
-    // fallback geometry: S stripes per failing query (S k <= kLKM for the final merge), at most
-    // kLKFail failing queries per scan launch
+    // fallback geometry: S stripes per failed query (S k <= kLKM for the final merge); the stripe
+    // lists of every query of a chunk have a slot (run), so the device needs no host decision
     const int S = (int)std::max<int64_t>(1, std::min<int64_t>({64, kLKM / k, (ix->ntotal + 1023) / 1024}));
     const int64_t R = (ix->ntotal + S - 1) / S;
-    constexpr int kLKFail = 64;
-    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)kLKFail * S * k)) != KNN_OK) return rc;
-    for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
-        const int64_t qc = std::min<int64_t>(kQueryChunk, nq - q0);
+    const int64_t chunk = std::min<int64_t>(kLKChunk, nq);
+    if ((rc = grow(&ix->lk_run, &ix->lk_run_cap, (size_t)chunk * S * k)) != KNN_OK) return rc;
+    // lk_fail: a chunk's failed queries [0, kLKChunk), their count, the search's total
+    if ((rc = grow(&ix->lk_fail, &ix->lk_fail_cap, (size_t)kLKChunk + 2)) != KNN_OK) return rc;
+    int* cnt = ix->lk_fail + kLKChunk;
+    KNN_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
+    for (int64_t q0 = 0; q0 < nq; q0 += kLKChunk) {
+        const int64_t qc = std::min<int64_t>(kLKChunk, nq - q0);
         const Plan p = make_plan(ix->ntotal, qc, KNN_MAX_K, ix->cus);     // KM = 32 lists
         // <= 4 queries whose rows fit the streaming pass's LDS: lists from one fp32 stream of the
         // corpus instead of 32-query tiles (IMGREC_STREAM_LISTS=0 at index creation: tiles)
@@ -498,7 +535,6 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         if ((rc = grow(&ix->qnorm, &ix->qnorm_cap, (size_t)p.nq_pad)) != KNN_OK) return rc;
         if ((rc = grow(&ix->cand_d, &ix->cand_d_cap, (size_t)qc * ncap)) != KNN_OK) return rc;
         if ((rc = grow(&ix->cand_i, &ix->cand_i_cap, (size_t)qc * ncap)) != KNN_OK) return rc;
-        if ((rc = grow(&ix->lk_fail, &ix->lk_fail_cap, (size_t)qc + 1)) != KNN_OK) return rc;
         KNN_HIP(launch_rows_ingest(q + q0 * ix->d, qc, ix->d, ix->dp, p.nq_pad,
                                    ix->metric == KNN_METRIC_COSINE ? 1 : 0, ix->qpad, ix->qnorm, st));
         int nlists = p.ncand / p.km, ncand = p.ncand;
@@ -517,27 +553,20 @@ int largek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
         }
         float* Db = D + q0 * k;
         int64_t* Ib = I + q0 * k;
-        int* cnt = ix->lk_fail + qc;
         KNN_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
         hipLaunchKernelGGL(largek_union_kernel, dim3((unsigned)qc), dim3(kLKThreads), 0, st, ix->cand_d,
                            ix->cand_i, nlists, KNN_MAX_K, ncand, k, ix->ntotal, kmetric,
-                           ix->id_offset, Db, Ib, ix->lk_fail, cnt);
+                           ix->id_offset, Db, Ib, ix->lk_fail, cnt, cnt + 1);
         KNN_HIP(hipGetLastError());
-        // the certificate's leftovers: the host reads their count (this path's only wait)
-        int nfail = 0;
-        KNN_HIP(hipMemcpyAsync(&nfail, cnt, sizeof(int), hipMemcpyDeviceToHost, st));
-        KNN_HIP(hipStreamSynchronize(st));
-        ix->lk_last_fallbacks += nfail;
-        for (int f0 = 0; f0 < nfail; f0 += kLKFail) {
-            const int nf = std::min(kLKFail, nfail - f0);
-            hipLaunchKernelGGL(largek_scan_kernel, dim3((unsigned)S, (unsigned)nf), dim3(kLKThreads), 0, st,
-                               ix->xb, ix->xn, ix->ntotal, ix->dp, ix->qpad, ix->qnorm, ix->lk_fail, f0, R,
-                               k, kmetric, ix->lk_run);
-            KNN_HIP(hipGetLastError());
-            hipLaunchKernelGGL(largek_final_kernel, dim3((unsigned)nf), dim3(kLKThreads), 0, st, ix->lk_run, S,
-                               k, ix->lk_fail, f0, kmetric, ix->id_offset, Db, Ib);
-            KNN_HIP(hipGetLastError());
-        }
+        // the certificate's leftovers, as many as the device counted: fixed grids walk them
+        const int G = (int)std::min<int64_t>(qc, kLKFailWG);
+        hipLaunchKernelGGL(largek_scan_kernel, dim3((unsigned)S, (unsigned)G), dim3(kLKThreads), 0, st,
+                           ix->xb, ix->xn, ix->ntotal, ix->dp, ix->qpad, ix->qnorm, ix->lk_fail, cnt, R,
+                           k, kmetric, ix->lk_run);
+        KNN_HIP(hipGetLastError());
+        hipLaunchKernelGGL(largek_final_kernel, dim3((unsigned)G), dim3(kLKThreads), 0, st, ix->lk_run, S,
+                           k, ix->lk_fail, cnt, kmetric, ix->id_offset, Db, Ib);
+        KNN_HIP(hipGetLastError());
     }
     return KNN_OK;
 }

@@ -312,8 +312,7 @@ int fan_out_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, i
     for (int s = 0; s < ndev; ++s) KNN_HIP(hipStreamWaitEvent(st, m->done[s], 0));
     const int kmetric = ix->metric == KNN_METRIC_L2 ? 1 : 0;
     if (k > KNN_MAX_K) {
-        if ((int64_t)ndev * k > 8192) KNN_FAIL(KNN_EINVAL, "k = %d over %d devices: at most 8192 entries per query", k, ndev);
-        KNN_HIP(launch_merge_large(m->gD, m->gI, ndev, nq, k, (int64_t)nk, (int64_t)nk, k, kmetric, D, I, st));
+        KNN_HIP(launch_merge_any(m->gD, m->gI, ndev, nq, k, (int64_t)nk, (int64_t)nk, k, kmetric, D, I, st));
         return KNN_OK;
     }
     KNN_HIP(launch_merge(m->gD, m->gI, nq, ndev, k, k, (int64_t)nk, k, kmetric, kmetric ? 0 : 1, D, I,

@@ -511,7 +511,8 @@ int search_locked(knn_index* ix, const float* q, int64_t nq, int k, float* D, in
     ix->stat_valid = false;
     if (k > KNN_MAX_K) {               // register top-k lists end at 32: faiss's GEMM + select form
         ix->last_path = 0;
-        return largek_search(ix, q, nq, k, D, I, st);
+        return k > KNN_MAX_K_LARGE ? hugek_search(ix, q, nq, k, D, I, st)
+                                   : largek_search(ix, q, nq, k, D, I, st);
     }
     if (ix->ntotal == 0) {
         KNN_HIP(launch_fill_empty(D, I, nq * (int64_t)k, kmetric, st));

@@ -282,7 +282,12 @@ vit_gemm_kernel(const uint32_t* __restrict__ xw, const uint32_t* __restrict__ ww
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (IMGREC_VIT_STORE_WAIT && s == 0 && prev_full)
+                // vmcnt(16): the youngest 16 vector-memory ops of a lane are the previous tile's 16
+                // output stores (one per 16-token block), so the stage's own DMA has landed.  Any
+                // epilogue that stores differently (the IMGREC_VIT_EPI_EXP measurement builds)
+                // waits for everything.
+                static_assert(kRB == 16, "vmcnt(16) counts one output store per 16-token block");
+                if (IMGREC_VIT_STORE_WAIT && IMGREC_VIT_EPI_EXP == 0 && s == 0 && prev_full)
                     asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

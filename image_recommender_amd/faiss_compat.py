@@ -157,8 +157,6 @@ class Index:
         k = int(k)
         if k <= 0:
             raise ValueError("k must be positive")
-        if k > KNN_MAX_K_LARGE:
-            raise NotImplementedError(f"k={k} exceeds the search limit of {KNN_MAX_K_LARGE}")
         n = x.shape[0]
         D = np.empty((n, k), dtype=np.float32) if D is None else D
         I = np.empty((n, k), dtype=np.int64) if I is None else I
@@ -235,7 +233,12 @@ class Index:
     def certificate_stats(self) -> dict:
         """The last search's certificate counts: queries on a candidate path, queries the second
         chance (all per-split list entries reranked) certified, queries re-run exactly, and the
-        largest observed error / bound.  Waits for that search to finish."""
+        largest observed error / bound.  Waits for that search to finish.
+
+        On the int8 direct route (batches of <= 4 queries, RerankArgs::direct: no merge and no
+        first rerank) every query goes straight to the second chance, so there `second_chance +
+        exact_reruns` equals the batch size by construction; it does not mean a first-pass
+        certificate failed."""
         a, b, c, r = C.c_int64(), C.c_int64(), C.c_int64(), C.c_float()
         _lib.check(_lib.load().knn_search_stats2(self._h, C.byref(a), C.byref(b), C.byref(c),
                                                  C.byref(r)), "knn_search_stats2")

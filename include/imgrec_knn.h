@@ -119,13 +119,15 @@ enum knn_search_mode {
 
 /* Largest k the fused top-k kernels serve (they keep per-lane lists of this length). */
 #define KNN_MAX_K 32
-/* Largest k one search can return: KNN_MAX_K < k <= KNN_MAX_K_LARGE runs the exact fp32 fused
- * kernel with 32-entry lists, the k best of their union by an exact per-query radix select,
- * certified against the lists' floor; the queries the certificate cannot settle are re-run by an
- * exact corpus scan (csrc/knn_largek.hip: no key block ever reaches HBM).  This is the one search
- * path that reads a count back to the host (device entry points included): once per 8192-query
- * chunk.  A multi-device index (knn_create_multi) runs it on every shard and merges the shards'
- * k-lists with the same select (at most 8192 gathered entries per query). */
+/* Every k >= 1 is served (faiss IndexFlat's range; past ntotal the tail is label -1, distance
+ * +-FLT_MAX).  KNN_MAX_K < k <= KNN_MAX_K_LARGE runs the exact fp32 fused kernel with 32-entry
+ * lists, the k best of their union by an exact per-query radix select, certified against the
+ * lists' floor; the queries the certificate cannot settle are re-run by an exact corpus scan whose
+ * fixed grid walks the failed queries the device counted (csrc/knn_largek.hip: no key block
+ * reaches HBM, the host never waits).  k > KNN_MAX_K_LARGE keys every (query, row) pair in fp32
+ * and sorts each query's keys (csrc/knn_hugek.hip: coverage of faiss's k range, not a fast path).
+ * Merges of k-lists (multi-device shards, knn_merge_*_device) use the in-LDS select up to 8192
+ * gathered entries per query and the sort beyond. */
 #define KNN_MAX_K_LARGE 1024
 
 /* Create an empty index of dimension d on HIP device `device` (-1 = current device). */

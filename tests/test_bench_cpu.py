@@ -36,6 +36,13 @@ def test_pmc_records_are_the_newest_matching(tmp_path, monkeypatch):
     rec, f = bench.pmc_record(pat, "_clock.json")
     assert f == "r01_v16_clock.json" and rec["clock_ghz"] == 1.7
     assert bench.pmc_traffic(r"no_such_kernel") is None
+    # config-2 records carry a workload tag: never cited for config 3, and the only ones for 2
+    (prof / "r01_v30_cfg2_traffic.json").write_text(json.dumps({kern: {"hbm_bytes_per_launch": 7.0}}))
+    (prof / "r01_v30_cfg2_clock.json").write_text(json.dumps({kern: {"clock_ghz": 1.8, "mfma_busy": 0.54}}))
+    assert bench.pmc_traffic(pat) == (2.0, "r01_v16_traffic.json")
+    assert bench.pmc_traffic(pat, "cfg2") == (7.0, "r01_v30_cfg2_traffic.json")
+    assert bench.pmc_record(pat, "_clock.json")[1] == "r01_v16_clock.json"
+    assert bench.pmc_record(pat, "_clock.json", "cfg2")[0]["mfma_busy"] == 0.54
 
 
 def test_committed_records_cover_the_bench_kernel():

@@ -134,3 +134,123 @@ def test_large_k_stream_pass_against_tiles_and_oracle(faiss, monkeypatch, metric
         out[name] = idx.search(xq, k)
         assert _fallbacks(idx) == 0, name
         check_knn(out[name][0], out[name][1], xb, xq, k, metric, min_exact_frac=0.5)
+
+
+def test_large_k_fallback_many_failed_queries_device_walk(faiss):
+    """More failed queries than the scan's fixed grid has workgroup rows (64) and than one chunk
+    holds (1,024): 1,500 queries with k = 900 of 1,000 rows — the lists hold fewer than k entries,
+    so every query goes to the exact scan, which walks the failed queries the device counted
+    (csrc/knn_largek.hip: no host read on the search path).  Every query against the oracle."""
+    xb = mixture(1000, 64, centres=20, seed=41)
+    xq = mixture(1500, 64, centres=20, seed=42)
+    idx = faiss.IndexFlatL2(64)
+    idx.add(xb)
+    D, I = idx.search(xq, 900)
+    assert _fallbacks(idx) == 1500
+    sel = np.random.default_rng(0).choice(1500, 40, replace=False)
+    check_knn(D[sel], I[sel], xb, xq[sel], 900, "l2", min_exact_frac=0.0)
+
+
+def test_large_k_search_never_waits_on_the_host(faiss):
+    """The large-k route on device pointers only enqueues work (it used to read the
+    failed-query count back per chunk, serialising a multi-device index's shards): a
+    device-pointer search captured into a HIP graph (a host read or stream sync would break the
+    capture) replays to the host search's exact result."""
+    import torch
+    from image_recommender_amd import _lib
+    xb = mixture(50_000, 64, centres=50, seed=43)
+    xq = torch.from_numpy(mixture(8, 64, centres=50, seed=44)).cuda()
+    idx = faiss.IndexFlatL2(64)
+    idx.add(xb)
+    k = 200
+    D = torch.empty((8, k), dtype=torch.float32, device="cuda")
+    I = torch.empty((8, k), dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    idx.search_device(xq.data_ptr(), 8, k, D.data_ptr(), I.data_ptr(), s.cuda_stream)   # workspace
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        idx.search_device(xq.data_ptr(), 8, k, D.data_ptr(), I.data_ptr(), s.cuda_stream)
+    D.zero_()
+    I.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    D2, I2 = idx.search(xq.cpu().numpy(), k)
+    np.testing.assert_array_equal(I.cpu().numpy(), I2)
+    np.testing.assert_array_equal(D.cpu().numpy(), D2)
+    assert _lib.load().knn_last_path(idx.handle) == 0
+
+
+# ------------------------------------------------------------------------------------------------
+# k > KNN_MAX_K_LARGE (csrc/knn_hugek.hip): every key, a segmented sort per query
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
+def test_huge_k_4096_on_100k_rows(faiss, metric):
+    """k = 4096 on 100k rows: labels and distances against the float64
+    oracle (rigorous + tight windows), 12 queries."""
+    n, d, k = 100_000, 128, 4096
+    xb = mixture(n, d, centres=100, seed=51)
+    xq = mixture(12, d, centres=100, seed=52)
+    mk = {"l2": faiss.IndexFlatL2, "ip": faiss.IndexFlatIP,
+          "cosine": lambda dd: faiss.IndexFlat(dd, faiss.METRIC_COSINE)}[metric]
+    idx = mk(d)
+    idx.add(xb)
+    D, I = idx.search(xq, k)
+    assert D.shape == (12, k) and (I >= 0).all()
+    check_knn(D, I, xb, xq, k, metric, min_exact_frac=0.5)
+
+
+def test_huge_k_whole_corpus_and_padding(faiss):
+    """k = ntotal orders the whole corpus exactly as the oracle (ties by label); k > ntotal pads
+    with label -1 and FLT_MAX (faiss IndexFlat's convention); duplicates tie by label."""
+    n, d = 3000, 48
+    xb = mixture(n, d, centres=10, seed=53)
+    xb[[5, 900, 2999]] = xb[100]
+    xq = mixture(4, d, centres=10, seed=54)
+    xq[0] = xb[100]
+    idx = faiss.IndexFlatL2(d)
+    idx.add(xb)
+    D, I = idx.search(xq, n)
+    assert sorted(I[1].tolist()) == list(range(n))
+    np.testing.assert_array_equal(I[0, :4], [5, 100, 900, 2999])
+    assert (D[0, :4] == 0.0).all()
+    check_knn(D, I, xb, xq, n, "l2", min_exact_frac=0.5)
+    D2, I2 = idx.search(xq, n + 500)
+    np.testing.assert_array_equal(I2[:, :n], I)
+    np.testing.assert_array_equal(D2[:, :n], D)
+    assert (I2[:, n:] == -1).all() and (D2[:, n:] == np.finfo(np.float32).max).all()
+
+
+def test_huge_k_multi_shard_index_and_packed_merge(faiss):
+    """k = 2000 over an 8-shard index (knn_create_multi on one device: 16,000 gathered entries per
+    query, beyond the in-LDS merge) and the packed all-gather merge of 8 row shards
+    (knn_merge_packed_device, sharded.py's layout): both equal the one-index search."""
+    import torch
+    from image_recommender_amd.sharded import merge_packed_device, packed_layout, packed_views, shard_range
+    n, d, k, nq = 40_000, 96, 2000, 6
+    xb = mixture(n, d, centres=40, seed=55)
+    xq = mixture(nq, d, centres=40, seed=56)
+    one = faiss.IndexFlatL2(d)
+    one.add(xb)
+    D1, I1 = one.search(xq, k)
+    multi = faiss.IndexFlatL2(d, devices=[0] * 8)
+    multi.add(xb)
+    Dm, Im = multi.search(xq, k)
+    np.testing.assert_array_equal(Im, I1)
+    np.testing.assert_array_equal(Dm, D1)
+    g = torch.zeros((8, packed_layout(nq, k)[0]), dtype=torch.uint8, device="cuda")
+    q = torch.from_numpy(xq).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    for r in range(8):
+        r0, r1 = shard_range(n, r, 8)
+        sh = faiss.IndexFlatL2(d)
+        sh.set_id_offset(r0)
+        sh.add(xb[r0:r1])
+        pD, pI = packed_views(g[r], nq, k)
+        sh.search_device(q.data_ptr(), nq, k, pD.data_ptr(), pI.data_ptr(), st)
+        torch.cuda.synchronize()
+    D, I = merge_packed_device(g, nq, k, k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(I.cpu().numpy(), I1)
+    np.testing.assert_array_equal(D.cpu().numpy(), D1)
+    check_knn(D1, I1, xb, xq, k, "l2", min_exact_frac=0.5)

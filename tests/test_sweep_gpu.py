@@ -109,13 +109,16 @@ def test_random_i8_case_matches_oracle(faiss, n, d, nq, k, metric, adds, seed):
     check_knn(D, I, xb, xq, k, metric, min_exact_frac=0.0)
 
 
-def test_k_above_limit_raises(faiss):
-    """k > KNN_MAX_K_LARGE is refused loudly."""
+def test_k_above_the_large_k_route(faiss):
+    """k > KNN_MAX_K_LARGE is served (faiss's range): 100 rows, k = 1025 — the 100 rows in the
+    oracle's order, then label -1 / FLT_MAX padding."""
     from image_recommender_amd._lib import KNN_MAX_K_LARGE
+    xb, xq = mixture(100, 64, seed=1), mixture(2, 64, seed=2)
     idx = faiss.IndexFlatL2(64)
-    idx.add(mixture(100, 64, seed=1))
-    with pytest.raises(NotImplementedError):
-        idx.search(mixture(2, 64, seed=2), KNN_MAX_K_LARGE + 1)
+    idx.add(xb)
+    D, I = idx.search(xq, KNN_MAX_K_LARGE + 1)
+    assert (I[:, 100:] == -1).all() and (D[:, 100:] == np.finfo(np.float32).max).all()
+    check_knn(D, I, xb, xq, KNN_MAX_K_LARGE + 1, "l2", min_exact_frac=0.5)
 
 
 @pytest.mark.parametrize("metric", ["l2", "ip", "cosine"])
