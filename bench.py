@@ -75,6 +75,10 @@ def parse():
                     help="only the timed steps (for rocprofv3 runs)")
     ap.add_argument("--no-phases", action="store_true",
                     help="skip the per-rank phase region (its event records show in kernel traces)")
+    ap.add_argument("--pmc", choices=("auto", "off"), default="auto",
+                    help="auto: at N = 1 on configs 2 / 3, measure the dominant kernel's HBM traffic, "
+                         "clock and MFMA busy in rocprofv3 --pmc passes of this same workload "
+                         "before the timed run (the committed profiles/ records otherwise)")
     return ap.parse_args()
 
 
@@ -312,8 +316,94 @@ def pmc_traffic(pattern: str, workload: str = ""):
     return None
 
 
+# ------------------------------------------------------------------------------------------------
+# live PMC passes (rocprofv3 child processes, started before this process touches the GPU)
+# ------------------------------------------------------------------------------------------------
+PMC_PASSES = {
+    "fetch": "FETCH_SIZE",
+    "write": "WRITE_SIZE",
+    "clock": "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA",
+}
+PMC_KERNELS = "knn_b16w_tile_kernel|knn_b16_tile_kernel|knn_tile_topk_kernel"
+
+
+def _pmc_rows(d: str):
+    import csv
+    import glob
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    return rows
+
+
+def live_pmc(a, budget_s: float = 150.0):
+    """Three rocprofv3 --pmc passes (FETCH_SIZE; WRITE_SIZE; GRBM_GUI_ACTIVE + SQ MFMA busy — one
+    pass each, within the per-pass block limits) over `bench.py --profile-only` of THIS workload,
+    as child processes (this process has not touched the GPU).  Returns {kernel name: record} with
+    the gfx950 corrections of MI355X_MICROARCH.md §HBM (read bytes = 2 x FETCH_SIZE KiB), or
+    ({}, reason) when rocprofv3 is missing or a pass fails."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return {}, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--profile-only", "--steps", "3", "--warmup", "1",
+             "--no-phases", "--pmc", "off", "--config", str(a.config), "--nq", str(a.nq), "--k", str(a.k),
+             "--mode", a.mode] + (["--rows", str(a.rows)] if a.rows else [])
+    env = dict(os.environ, TMPDIR="/tmp")
+    out = tempfile.mkdtemp(prefix="imgrec_pmc_", dir="/tmp")
+    t0 = time.perf_counter()
+    recs = {}
+    for name, counters in PMC_PASSES.items():
+        left = budget_s - (time.perf_counter() - t0)
+        if left < 20:
+            return {}, f"PMC budget ({budget_s:.0f} s) spent before the {name} pass"
+        cmd = [prof, "--kernel-trace", "--kernel-include-regex", PMC_KERNELS, "--pmc", *counters.split(),
+               "-d", os.path.join(out, name), "-o", "run", "--output-format", "csv", "--"] + child
+        p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                             text=True, start_new_session=True)
+        try:
+            _, err = p.communicate(timeout=min(left, 90.0))
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return {}, f"rocprofv3 {name} pass timed out"
+        if p.returncode != 0:
+            return {}, f"rocprofv3 {name} pass exited {p.returncode}: {err.strip()[-200:]}"
+        rows = _pmc_rows(os.path.join(out, name))
+        if not rows:
+            return {}, f"rocprofv3 {name} pass wrote no counter rows"
+        for r in rows:
+            k = r["Kernel_Name"].split("(")[0]
+            rec = recs.setdefault(k, {})
+            rec.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            if name == "clock":
+                rec.setdefault("_dur", []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    res = {}
+    for k, rec in recs.items():
+        if "FETCH_SIZE" not in rec or "WRITE_SIZE" not in rec or "GRBM_GUI_ACTIVE" not in rec:
+            continue
+        mean = lambda v: sum(v) / len(v)                 # noqa: E731
+        fetch, write = mean(rec["FETCH_SIZE"]), mean(rec["WRITE_SIZE"])
+        t = mean(rec["_dur"])
+        clk = mean(rec["GRBM_GUI_ACTIVE"]) / 8 / t       # cycles per XCD over the kernel
+        busy = mean(rec["SQ_VALU_MFMA_BUSY_CYCLES"]) / (256 * 4 * clk * t)
+        res[k] = {"hbm_bytes_per_launch": 2 * fetch * 1024 + write * 1024, "hbm_read_bytes": 2 * fetch * 1024,
+                  "hbm_write_bytes": write * 1024, "launches": len(rec["FETCH_SIZE"]),
+                  "clock_ghz": clk / 1e9, "mfma_busy": busy, "dur_ms_under_pmc": t * 1e3}
+    shutil.rmtree(out, ignore_errors=True)
+    return res, f"{len(PMC_PASSES)} rocprofv3 --pmc passes of this workload, {time.perf_counter() - t0:.0f} s"
+
+
 def main():
     a = parse()
+    live = None
+    if (a.pmc == "auto" and a.gpus == 1 and "WORLD_SIZE" not in os.environ and not a.profile_only
+            and a.config in (2, 3)):
+        live = live_pmc(a)
+        print(f"[bench] live PMC: {live[1]}", file=sys.stderr, flush=True)
     # --gpus N > 1 without torchrun: start the N ranks here (no device touched in this process)
     # or stop with a non-zero status; never a silent one-GPU run (image_recommender_amd/launch.py)
     from image_recommender_amd.launch import maybe_spawn
@@ -480,20 +570,24 @@ def main():
     torch.cuda.synchronize()
     el1, _, _ = region(lambda: shard.search(q1, a.k), a.single_query_steps, False)
     _, kern1_ms, _ = region(lambda: shard.search(q1, a.k), a.single_query_steps, True)
-    # cold: every search right after a 512 MiB copy (512 MiB read + 512 MiB written), more than
-    # the 256 MB MALL (Infinity Cache) and the L2s hold, so no corpus line survives from the
-    # previous search — the reference CLI's one query arrives cold.  The copy's own time is
-    # measured alone and subtracted; the kernel's duration comes from its own events.
-    flush_src = torch.empty(512 << 20, dtype=torch.uint8, device=device).fill_(1)
-    flush_dst = torch.empty_like(flush_src)
+    # cold: every search right after a read of a 512 MiB buffer, more than the 256 MB MALL
+    # (Infinity Cache) and the L2s hold, so no corpus line survives from the previous search —
+    # the reference CLI's one query arrives cold.  A read (a sum) leaves no dirty lines to drain
+    # under the search.  The flush's own time is measured alone and subtracted; the kernel's
+    # duration comes from its own events.
+    flush_buf = torch.ones(128 << 20, dtype=torch.int32, device=device)
+    flush_out = torch.empty((), dtype=torch.int64, device=device)
+
+    def flush():
+        torch.sum(flush_buf, dtype=torch.int64, out=flush_out)
 
     def cold_search():
-        flush_dst.copy_(flush_src)
+        flush()
         return shard.search(q1, a.k)
-    el_flush, _, _ = region(lambda: flush_dst.copy_(flush_src), a.single_query_steps, False)
+    el_flush, _, _ = region(flush, a.single_query_steps, False)
     el1c, _, _ = region(cold_search, a.single_query_steps, False)
     _, kern1c_ms, _ = region(cold_search, a.single_query_steps, True)
-    del flush_src, flush_dst
+    del flush_buf, flush_out
     path1 = lib.knn_last_path(h)                               # 0 exact, 1 split, 2 bf16, 3 i8
 
     tr, tq, sp, wg = C.c_int(), C.c_int(), C.c_int(), C.c_int()
@@ -516,6 +610,13 @@ def main():
                    and a.k == 10)
         wl = "" if a.config == 3 else f"cfg{a.config}"
         traffic = pmc_traffic(kpat, wl) if pmc_run else None
+        busy = pmc_record(kpat, "_clock.json", wl) if pmc_run else None
+        import re
+        live_rec = next((r for kn, r in (live[0] if live else {}).items() if re.search(kpat, kn)), None)
+        if live_rec is not None:
+            src = f"live: {live[1]}"
+            traffic = (live_rec["hbm_bytes_per_launch"], src)
+            busy = (live_rec, src)
         achieved = flops / (kern_ms * 1e-3) / 1e12
         # matrix-pipe ceiling for the algorithmic 2NDQ flop: bf16 path one bf16 MFMA per product
         # (bf16 dense peak); split path three (hi.hi + hi.lo + lo.hi: bf16 peak / 3); exact path
@@ -533,7 +634,6 @@ def main():
         # the fp32 rows
         stream1 = ({3: 1.0 * n_local * dpb + 4.0 * n_local * (dpb // 64), 2: 2.0 * n_local * dpb}
                    .get(path1, 4.0 * n_local * D_total) + 4.0 * n_local)
-        busy = pmc_record(kpat, "_clock.json", wl) if pmc_run else None
         qps = a.nq * a.steps / elapsed
         out = {
             "metric": "k-NN queries/sec + recall@10 on 1M concat vectors at 1/2/4/8 MI355X",
@@ -579,6 +679,8 @@ def main():
                 "mfma_busy": busy[0]["mfma_busy"] if busy else None,
                 "clock_ghz": busy[0]["clock_ghz"] if busy else None,
                 "busy_source": busy[1] if busy else None,
+                "pmc_live": (live[1] if live else "not run (--pmc off, N > 1 or a config without "
+                                                  "records)") if rank == 0 else None,
                 "algorithmic": f"2*N*D*Q = 2*{n_local}*{D_total}*{nq_local} flop per launch",
             },
             "single_query": {
@@ -586,7 +688,7 @@ def main():
                 "ms_per_query_cold": max(el1c - el_flush, 0.0) / a.single_query_steps * 1e3,
                 "kernel_ms": kern1_ms,
                 "kernel_ms_cold": kern1c_ms,
-                "cache_state": ("hbm_gbs / hbm_frac: cold (each search after a 512 MiB copy "
+                "cache_state": ("hbm_gbs / hbm_frac: cold (each search after a 512 MiB read "
                                 "evicts the 256 MB MALL and the L2s); *_warm: back-to-back "
                                 "searches of the same resident corpus"),
                 "path": {0: "exact", 1: "split", 2: "bf16", 3: "i8"}.get(path1, "?"),
