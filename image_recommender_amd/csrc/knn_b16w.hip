@@ -73,14 +73,17 @@ static_assert(kBKW == 32 && kCPR == 8, "stage depth: two 32-deep k-steps per sta
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
 static_assert(kDeferQ >= 0 && kDeferQ < kQuads - 1, "deferred DMA inside the stage's first quads");
-// Screen early-out (A/B): per row group first the lane minimum of the screen values, two rows per
-// v_pk_min, and the per-row sign masks only when some lane of the wave has a passing row (the
-// full test is a superset check: rows at exactly the threshold take the full path)
-#ifndef IMGREC_B16W_SCREEN_MIN
-#define IMGREC_B16W_SCREEN_MIN 0
+// Insertion without the LDS park (A/B): a passing row's accumulator and norm are picked from the
+// registers of its two row blocks by a 3-level v_cndmask tree instead of a ds_write / ds_read
+// round trip per row (the norms stay in the registers the screen loaded them into)
+#ifndef IMGREC_B16W_NOPARK
+#define IMGREC_B16W_NOPARK 0
 #endif
 // Measurement builds only (tools/b16w_epi_split.sh; the lists they return are wrong):
-// 1 = no per-tile epilogue (the stage loop alone), 2 = the screen without the insertions
+// 1 = no per-tile epilogue (the stage loop alone), 2 = the screen without the insertions.  Both
+// hand every accumulator (and 2 the screen's masks) to an empty asm at each tile end, so the
+// MFMAs and the screen stay live (round 6: without it the compiler dropped every MFMA — PMC
+// SQ_INSTS_MFMA = 0, profiles/r06/epi_split/pmc_invalid_variants/).
 #ifndef IMGREC_B16W_EPI_EXP
 #define IMGREC_B16W_EPI_EXP 0
 #endif
@@ -158,6 +161,14 @@ __device__ __forceinline__ uint32_t ord_bits(float k) {
 }
 __device__ __forceinline__ float ord_float(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+// x[r] of eight register values, r in [0, 8) (lane-varying): three levels of v_cndmask
+__device__ __forceinline__ float sel8(int r, float x0, float x1, float x2, float x3, float x4, float x5,
+                                      float x6, float x7) {
+    const bool b0 = r & 1, b1 = r & 2, b2 = r & 4;
+    const float a0 = b0 ? x1 : x0, a1 = b0 ? x3 : x2, a2 = b0 ? x5 : x4, a3 = b0 ? x7 : x6;
+    const float c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+    return b2 ? c1 : c0;
 }
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return max(min(a, b), min(max(a, b), c));          // -> v_med3_u32
@@ -425,6 +436,12 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
         // The test runs on the accumulator (see knn_b16.hip): d = (|x|^2 (1/2 - 2^-20) + c) - acc
         // with c = (|q|^2 - T)/2 - 2^-20 (|q|^2 + |T|) is negative iff the row passes.
         B16W_STAMP(2 * (t - t0));
+#if IMGREC_B16W_EPI_EXP != 0
+#pragma unroll
+        for (int rb = 0; rb < kRB; ++rb)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) asm volatile("" :: "v"(acc[rb][h]));
+#endif
         const float* nrm = reinterpret_cast<const float*>(smem + kNormOff + ((t - t0) % kNormSlots) * kBM * 4);
         const bool full = (t + 1) * kGPT <= cnt && trow(t, kBM - 1) < nrows;
         auto row_ok = [&](int tr) { return t * kGPT + tr / kRPP < cnt && trow(t, tr) < nrows; };
@@ -445,28 +462,6 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
             // row group rg = row blocks 4 rg .. 4 rg + 3; bit 4 j + i of a mask = accumulator
             // register i of row block 4 rg + j = tile row (4 rg + j) * 16 + 4 lq + i
             screen();
-#if IMGREC_B16W_SCREEN_MIN
-            {
-                f32x2 mn[2] = {(f32x2){INFINITY, INFINITY}, (f32x2){INFINITY, INFINITY}};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int rb = 4 * rg + j;
-                    float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (L2) n4 = *reinterpret_cast<const float4*>(nrm + rb * 16 + 4 * lq);
-                    const f32x2 half2 = (f32x2){0.5f - kLo, 0.5f - kLo};
-                    const f32x2 hlo = (f32x2){n4.x, n4.y} * half2, hhi = (f32x2){n4.z, n4.w} * half2;
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const f32x2 c2 = (f32x2){cth[h], cth[h]};
-                        const f32x2 dhi = (L2 ? hhi + c2 : c2) - (f32x2){acc[rb][h][2], acc[rb][h][3]};
-                        const f32x2 dlo = (L2 ? hlo + c2 : c2) - (f32x2){acc[rb][h][0], acc[rb][h][1]};
-                        mn[h] = __builtin_elementwise_min(mn[h], __builtin_elementwise_min(dhi, dlo));
-                    }
-                }
-                const f32x2 m2 = __builtin_elementwise_min(mn[0], mn[1]);
-                if (!__any(fminf(m2.x, m2.y) <= 0.f)) continue;    // no row of the group passes
-            }
-#endif
             unsigned live = 0xffffu;
             if (!full) {
                 live = 0;
@@ -474,11 +469,13 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                 for (int b = 0; b < 16; ++b) live |= (unsigned)row_ok((4 * rg + (b >> 2)) * 16 + 4 * lq + (b & 3)) << b;
             }
             unsigned msk[2] = {0u, 0u};
+            float4 nr4[4];                                      // the group's row norms
 #pragma unroll
             for (int j = 3; j >= 0; --j) {                      // high bits first
                 const int rb = 4 * rg + j;
                 float4 n4 = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (L2) n4 = *reinterpret_cast<const float4*>(nrm + rb * 16 + 4 * lq);
+                nr4[j] = n4;
                 const f32x2 half2 = (f32x2){0.5f - kLo, 0.5f - kLo};
                 const f32x2 hlo = (f32x2){n4.x, n4.y} * half2, hhi = (f32x2){n4.z, n4.w} * half2;
 #pragma unroll
@@ -496,9 +493,7 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
             const unsigned long long ins0 = __builtin_amdgcn_s_memtime();
 #endif
 #if IMGREC_B16W_EPI_EXP == 2
-            // (keep the screen live: fold its masks into list entry 0, never an insertion)
-            kp[0][0] ^= (msk[0] & live) & 0x80000000u;
-            kp[1][0] ^= (msk[1] & live) & 0x80000000u;
+            asm volatile("" :: "v"(msk[0] & live), "v"(msk[1] & live));   // the screen, no insertion
             continue;
 #endif
 #pragma unroll
@@ -510,9 +505,11 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                     unsigned mh = (m >> (8 * hf)) & 0xffu;
                     if (!__any(mh != 0)) continue;
                     const int rb0 = 4 * rg + 2 * hf;
+#if !IMGREC_B16W_NOPARK
                     park[lane] = make_float4(acc[rb0][h][0], acc[rb0][h][1], acc[rb0][h][2], acc[rb0][h][3]);
                     park[64 + lane] = make_float4(acc[rb0 + 1][h][0], acc[rb0 + 1][h][1],
                                                   acc[rb0 + 1][h][2], acc[rb0 + 1][h][3]);
+#endif
                     while (__any(mh != 0)) {
 #ifdef IMGREC_B16_STAMPS
                         ++nit;
@@ -520,9 +517,18 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
                         const bool act = mh != 0u;
                         const int r8 = act ? __builtin_ctz(mh) : 0;
                         mh &= mh - 1u;
-                        const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
                         const int tr = (rb0 + (r8 >> 2)) * 16 + 4 * lq + (r8 & 3);
-                        float kv = L2 ? fmaf(-2.f, a, qn[h] + nrm[tr]) : -a;
+#if IMGREC_B16W_NOPARK
+                        const float a = sel8(r8, acc[rb0][h][0], acc[rb0][h][1], acc[rb0][h][2], acc[rb0][h][3],
+                                             acc[rb0 + 1][h][0], acc[rb0 + 1][h][1], acc[rb0 + 1][h][2],
+                                             acc[rb0 + 1][h][3]);
+                        const float4 na = nr4[2 * hf], nb = nr4[2 * hf + 1];
+                        const float xn = L2 ? sel8(r8, na.x, na.y, na.z, na.w, nb.x, nb.y, nb.z, nb.w) : 0.f;
+#else
+                        const float a = pk[((r8 >> 2) * 64 + lane) * 4 + (r8 & 3)];
+                        const float xn = L2 ? nrm[tr] : 0.f;
+#endif
+                        float kv = L2 ? fmaf(-2.f, a, qn[h] + xn) : -a;
                         if constexpr (PACK) {
                             // L2: the clamp at 0 and the order map in two integer ops — a key
                             // with the sign bit set (negative or -0) maps to ord(+0) = 2^31, a

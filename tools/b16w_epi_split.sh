@@ -8,7 +8,7 @@
 set -u
 OUT=$1; shift
 mkdir -p $OUT
-for v in ${LIBS:-libimgrec.so libimgrec_noepi.so libimgrec_scronly.so libimgrec_scrmin.so}; do
+for v in ${LIBS:-libimgrec.so libimgrec_noepi.so libimgrec_scronly.so}; do
   IMGREC_LIB_NAME=$v timeout -k 10 300 python3 bench.py --profile-only --steps 20 --warmup 3 --no-phases "$@" \
       > $OUT/$v.json 2> $OUT/$v.err || { echo "$v failed"; tail -5 $OUT/$v.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('$OUT/$v.json')); print('$v', 'kernel_ms %.4f' % d['kernel_ms'], 'ms_per_step %.4f' % d['ms_per_step'])"
