@@ -400,8 +400,10 @@ def live_pmc(a, budget_s: float = 150.0):
 def main():
     a = parse()
     live = None
+    # (not under a profiler already: rocprofv3 exports ROCPROF_* to the program it runs)
+    profiled = any(k.startswith("ROCPROF") for k in os.environ)
     if (a.pmc == "auto" and a.gpus == 1 and "WORLD_SIZE" not in os.environ and not a.profile_only
-            and a.config in (2, 3)):
+            and a.config in (2, 3) and not profiled):
         live = live_pmc(a)
         print(f"[bench] live PMC: {live[1]}", file=sys.stderr, flush=True)
     # --gpus N > 1 without torchrun: start the N ranks here (no device touched in this process)

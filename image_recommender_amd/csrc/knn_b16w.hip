@@ -73,11 +73,13 @@ static_assert(kBKW == 32 && kCPR == 8, "stage depth: two 32-deep k-steps per sta
 static_assert(kLDS <= 160 * 1024, "LDS budget");
 static_assert(kLPW % 4 == 0, "pieces go out in dma4x groups of four");
 static_assert(kDeferQ >= 0 && kDeferQ < kQuads - 1, "deferred DMA inside the stage's first quads");
-// Insertion without the LDS park (A/B): a passing row's accumulator and norm are picked from the
-// registers of its two row blocks by a 3-level v_cndmask tree instead of a ds_write / ds_read
-// round trip per row (the norms stay in the registers the screen loaded them into)
+// Insertion without the LDS park (round 6 default; =0 restores the park for A/B): a passing row's
+// accumulator and norm are picked from the registers of its two row blocks by a 3-level
+// v_cndmask tree instead of a ds_write / ds_read round trip per row (the norms stay in the
+// registers the screen loaded them into).  Bit-identical; cfg2 0.3-1.2 % faster, cfg3 the same
+// (profiles/r06/nopark/).
 #ifndef IMGREC_B16W_NOPARK
-#define IMGREC_B16W_NOPARK 0
+#define IMGREC_B16W_NOPARK 1
 #endif
 // Measurement builds only (tools/b16w_epi_split.sh; the lists they return are wrong):
 // 1 = no per-tile epilogue (the stage loop alone), 2 = the screen without the insertions.  Both
