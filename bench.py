@@ -581,7 +581,7 @@ def main():
     flush_out = torch.empty((), dtype=torch.int64, device=device)
 
     def flush():
-        torch.sum(flush_buf, dtype=torch.int64, out=flush_out)
+        torch.sum(flush_buf, dim=0, dtype=torch.int64, out=flush_out)
 
     def cold_search():
         flush()
