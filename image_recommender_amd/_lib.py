@@ -52,6 +52,8 @@ SIGNATURES = {
     # imgrec_ivfpq.h
     "ivfpq_lut_device": (_i, [_vp, _i64, _i, _i, _i, _vp, _vp, _vp]),
     "ivfpq_scan_device": (_i, [_vp, _vp, _i64, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "ivfpq_scan_all_device": (_i, [_vp, _vp, _i64, _i, _vp, _vp, _vp, _i, _i, _vp, _vp, _i64, _i, _vp,
+                                   _vp, _vp]),
     "knn_write": (_i, [_vp, C.c_char_p]),
     "knn_read": (_i, [C.c_char_p, _i, C.POINTER(_vp)]),
     "knn_read_multi": (_i, [C.c_char_p, _pi, _i, C.POINTER(_vp)]),

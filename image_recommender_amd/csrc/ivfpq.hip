@@ -25,6 +25,8 @@
 #include <float.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "knn_kernels.h"
 #include "wave_ops.h"
 
@@ -142,7 +144,74 @@ ivfpq_scan_kernel(const float* __restrict__ lut, const int64_t* __restrict__ pro
     }
 }
 
+// Any k (faiss IndexIVFPQ serves every k): the ADC distance of EVERY row of each query's probed
+// lists, summed in the scan kernel's order (the same bits), as (ordered key bits << 32 | label) at
+// the (query, probe)'s slot probe_off[q * nprobe + p]; a segmented sort per query follows.
+__global__ void __launch_bounds__(256)
+ivfpq_adc_all_kernel(const float* __restrict__ lut, const int64_t* __restrict__ probes,
+                     const int64_t* __restrict__ list_off, const uint16_t* __restrict__ codes,
+                     const int64_t* __restrict__ ids, int m, int ksub,
+                     const int64_t* __restrict__ probe_off, uint64_t* __restrict__ out) {
+    const int64_t qp = blockIdx.x;                              // q * nprobe + p
+    const int64_t l = probes[qp];
+    if (l < 0) return;
+    const float* T = lut + (size_t)qp * m * ksub;
+    const int64_t r0 = list_off[l], r1 = list_off[l + 1];
+    uint64_t* o = out + probe_off[qp];
+    for (int64_t row = r0 + threadIdx.x; row < r1; row += 256) {
+        const uint16_t* c = codes + row * m;
+        float dist = 0.f;
+        for (int j = 0; j < m; ++j) dist += T[(size_t)j * ksub + c[j]];
+        o[row - r0] = ((uint64_t)key_bits_ordered(dist) << 32) | (uint32_t)ids[row];
+    }
+}
+
+// Row q of D / I: the first min(k, segment size) sorted entries of query q, then -1 / FLT_MAX.
+__global__ void ivfpq_write_all_kernel(const uint64_t* __restrict__ sorted, const uint32_t* __restrict__ seg_off,
+                                       int k, float* __restrict__ D, int64_t* __restrict__ I) {
+    const int64_t q = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= k) return;
+    const int64_t n = (int64_t)seg_off[q + 1] - seg_off[q];
+    const uint64_t x = i < n ? sorted[seg_off[q] + i] : ~0ull;
+    D[q * k + i] = x == ~0ull ? FLT_MAX : key_from_ordered((uint32_t)(x >> 32));
+    I[q * k + i] = x == ~0ull ? (int64_t)-1 : (int64_t)(uint32_t)x;
+}
+
 }  // namespace
+
+hipError_t launch_ivfpq_scan_all(const float* lut, const int64_t* probes, int64_t nq, int nprobe,
+                                 const int64_t* list_off, const uint16_t* codes, const int64_t* ids,
+                                 int m, int ksub, const int64_t* probe_off, const uint32_t* seg_off,
+                                 int64_t total, int k, float* D, int64_t* I, hipStream_t st) {
+    if (nq <= 0) return hipSuccess;
+    if (k <= 0 || nprobe <= 0 || m <= 0 || ksub <= 0 || ksub > 65536 || total < 0 ||
+        total >= ((int64_t)1 << 32) || nq > 0x7fffffff)
+        return hipErrorInvalidValue;
+    uint64_t *a = nullptr, *b = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_cap = 0;
+    hipError_t e = hipSuccess;
+    const size_t nbytes = (size_t)std::max<int64_t>(total, 1) * 8;
+    if ((e = hipMallocAsync((void**)&a, nbytes, st)) == hipSuccess &&
+        (e = hipMallocAsync((void**)&b, nbytes, st)) == hipSuccess) {
+        if (total > 0) {
+            hipLaunchKernelGGL(ivfpq_adc_all_kernel, dim3((unsigned)(nq * nprobe)), dim3(256), 0, st, lut,
+                               probes, list_off, codes, ids, m, ksub, probe_off, a);
+            e = hipGetLastError();
+            if (e == hipSuccess)
+                e = sort_u64_segments(a, b, total, (int)nq, seg_off, 64u, &tmp, &tmp_cap, true, st);
+        }
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(ivfpq_write_all_kernel, dim3((unsigned)((k + 255) / 256), (unsigned)nq), dim3(256),
+                               0, st, b, seg_off, k, D, I);
+            e = hipGetLastError();
+        }
+    }
+    for (void* p : {(void*)a, (void*)b, tmp})
+        if (p) (void)hipFreeAsync(p, st);
+    return e;
+}
 
 hipError_t launch_ivfpq_lut(const float* resid, int64_t nr, int d, int m, int ksub,
                             const float* cbt, float* lut, hipStream_t st) {

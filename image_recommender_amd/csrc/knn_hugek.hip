@@ -154,8 +154,16 @@ hipError_t sort_segments(uint64_t* in, uint64_t* out, int nseg, int64_t seg, uns
                        nseg, seg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    return sort_u64_segments(in, out, (int64_t)nseg * seg, nseg, off, end_bit, tmp, tmp_cap, async_tmp, st);
+}
+
+}  // namespace
+
+hipError_t sort_u64_segments(uint64_t* in, uint64_t* out, int64_t total, int nseg, const unsigned* off,
+                             unsigned end_bit, void** tmp, size_t* tmp_cap, bool async_tmp, hipStream_t st) {
+    hipError_t e;
     size_t need = 0;
-    e = rocprim::segmented_radix_sort_keys(nullptr, need, in, out, (unsigned)(nseg * seg), (unsigned)nseg,
+    e = rocprim::segmented_radix_sort_keys(nullptr, need, in, out, (unsigned)total, (unsigned)nseg,
                                            off, off + 1, 0u, end_bit, st);
     if (e != hipSuccess) return e;
     if (need > *tmp_cap) {
@@ -166,11 +174,9 @@ hipError_t sort_segments(uint64_t* in, uint64_t* out, int nseg, int64_t seg, uns
         *tmp_cap = need;
     }
     size_t have = *tmp_cap;
-    return rocprim::segmented_radix_sort_keys(*tmp, have, in, out, (unsigned)(nseg * seg), (unsigned)nseg,
+    return rocprim::segmented_radix_sort_keys(*tmp, have, in, out, (unsigned)total, (unsigned)nseg,
                                               off, off + 1, 0u, end_bit, st);
 }
-
-}  // namespace
 
 int hugek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int64_t* I,
                  hipStream_t st) {

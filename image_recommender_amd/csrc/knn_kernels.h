@@ -306,6 +306,16 @@ hipError_t launch_query_prep_b16(const float* src, int64_t n, int d, int dp, int
 hipError_t launch_max_norm(const float* xn, int64_t n, float* out, hipStream_t st);
 
 // IVF-PQ (ivfpq.hip; layouts in include/imgrec_ivfpq.h)
+// segmented radix sort of u64 keys (knn_hugek.hip, rocPRIM): segment i = [off[i], off[i + 1]) of
+// `total` (< 2^32) keys over bits [0, end_bit); the temporary storage grows in *tmp (hipMallocAsync
+// on st when async_tmp)
+hipError_t sort_u64_segments(uint64_t* in, uint64_t* out, int64_t total, int nseg, const unsigned* off,
+                             unsigned end_bit, void** tmp, size_t* tmp_cap, bool async_tmp, hipStream_t st);
+// IVF-PQ for any k: every probed row's ADC key, a segmented sort per query, the first k
+hipError_t launch_ivfpq_scan_all(const float* lut, const int64_t* probes, int64_t nq, int nprobe,
+                                 const int64_t* list_off, const uint16_t* codes, const int64_t* ids,
+                                 int m, int ksub, const int64_t* probe_off, const uint32_t* seg_off,
+                                 int64_t total, int k, float* D, int64_t* I, hipStream_t st);
 hipError_t launch_ivfpq_lut(const float* resid, int64_t nr, int d, int m, int ksub,
                             const float* cbt, float* lut, hipStream_t st);
 hipError_t launch_ivfpq_scan(const float* lut, const int64_t* probes, int64_t nq, int nprobe,

@@ -216,13 +216,14 @@ class IndexIVFPQ:
         self._list_off[1:] = torch.cumsum(cnt, 0)
 
     def search(self, x, k: int):
-        """(D, I) numpy (nq, k): squared-L2 ADC distances ascending, ties by the smaller label."""
+        """(D, I) numpy (nq, k): squared-L2 ADC distances ascending, ties by the smaller label; any k
+        (k <= 32: per-lane register lists; beyond: every probed row keyed and sorted per query)."""
         torch = _torch()
         if not self.is_trained:
             raise RuntimeError("Error in search: index is not trained")
         k = int(k)
-        if not 1 <= k <= KNN_MAX_K:
-            raise NotImplementedError(f"k must be in [1, {KNN_MAX_K}]")
+        if k < 1:
+            raise ValueError("k must be positive")
         q = self._tensor(x)
         nq, npb = q.shape[0], max(1, min(int(self.nprobe), self.nlist))
         D = torch.empty((nq, k), dtype=torch.float32, device=self.device)
@@ -242,13 +243,36 @@ class IndexIVFPQ:
                                             self.m, self.ksub, C.c_void_p(self._cbt.data_ptr()),
                                             C.c_void_p(lut.data_ptr()), C.c_void_p(st)),
                        "ivfpq_lut_device")
-            _lib.check(lib.ivfpq_scan_device(C.c_void_p(lut.data_ptr()), C.c_void_p(probes.data_ptr()),
-                                             q1 - q0, npb, C.c_void_p(self._list_off.data_ptr()),
-                                             C.c_void_p(self._codes.data_ptr()),
-                                             C.c_void_p(self._ids.data_ptr()), self.m, self.ksub, k,
-                                             C.c_void_p(D[q0:q1].data_ptr()),
-                                             C.c_void_p(I[q0:q1].data_ptr()), C.c_void_p(st)),
-                       "ivfpq_scan_device")
+            if k <= KNN_MAX_K:      # register top-k lists per lane (ivfpq_scan_kernel)
+                _lib.check(lib.ivfpq_scan_device(C.c_void_p(lut.data_ptr()), C.c_void_p(probes.data_ptr()),
+                                                 q1 - q0, npb, C.c_void_p(self._list_off.data_ptr()),
+                                                 C.c_void_p(self._codes.data_ptr()),
+                                                 C.c_void_p(self._ids.data_ptr()), self.m, self.ksub, k,
+                                                 C.c_void_p(D[q0:q1].data_ptr()),
+                                                 C.c_void_p(I[q0:q1].data_ptr()), C.c_void_p(st)),
+                           "ivfpq_scan_device")
+                continue
+            # any k: every probed row's ADC key, sorted per query (ivfpq_scan_all_device); the
+            # slots of each (query, probe) and each query come from the probed lists' sizes
+            pr = probes.reshape(-1)
+            cnt = torch.where(pr >= 0, self._list_off[pr.clamp_min(0) + 1] - self._list_off[pr.clamp_min(0)],
+                              torch.zeros_like(pr))
+            probe_off = (torch.cumsum(cnt, 0) - cnt).contiguous()
+            total = int(cnt.sum())
+            qoff = torch.cat([probe_off.reshape(q1 - q0, npb)[:, 0],
+                              torch.tensor([total], dtype=torch.int64, device=self.device)])
+            if total >= 2 ** 32:
+                raise ValueError("IVF-PQ search: more than 2^32 probed entries in one chunk")
+            seg_off = qoff.to(torch.int32).contiguous()     # (the int32 bits are the uint32 offsets)
+            _lib.check(lib.ivfpq_scan_all_device(C.c_void_p(lut.data_ptr()), C.c_void_p(probes.data_ptr()),
+                                                 q1 - q0, npb, C.c_void_p(self._list_off.data_ptr()),
+                                                 C.c_void_p(self._codes.data_ptr()),
+                                                 C.c_void_p(self._ids.data_ptr()), self.m, self.ksub,
+                                                 C.c_void_p(probe_off.data_ptr()),
+                                                 C.c_void_p(seg_off.data_ptr()), total, k,
+                                                 C.c_void_p(D[q0:q1].data_ptr()),
+                                                 C.c_void_p(I[q0:q1].data_ptr()), C.c_void_p(st)),
+                       "ivfpq_scan_all_device")
         torch.cuda.synchronize(self.device)
         return D.cpu().numpy(), I.cpu().numpy()
 

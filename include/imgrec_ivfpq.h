@@ -41,6 +41,18 @@ int ivfpq_scan_device(const float* lut, const int64_t* probes, int64_t nq, int n
                       const int64_t* list_off, const uint16_t* codes, const int64_t* ids, int m,
                       int ksub, int k, float* D, int64_t* I, void* stream);
 
+/* Any k (faiss IndexIVFPQ's range): the ADC distance of every row of each query's probed lists
+ * (summed as ivfpq_scan_device sums it), sorted per query by (distance, label), the first k, then
+ * label -1 / FLT_MAX.  probe_off (nq x nprobe int64): the first slot of (query q, probe p) in a
+ * buffer of `total` entries, the rows of that probe's list in list order (0 rows for a -1 probe);
+ * seg_off (nq + 1 uint32): query q's entries are [seg_off[q], seg_off[q + 1]), seg_off[nq] =
+ * total < 2^32.  Labels < 2^32.  Work space (2 x total x 8 B + the sort's) is allocated and freed
+ * in stream order on `stream`. */
+int ivfpq_scan_all_device(const float* lut, const int64_t* probes, int64_t nq, int nprobe,
+                          const int64_t* list_off, const uint16_t* codes, const int64_t* ids, int m,
+                          int ksub, const int64_t* probe_off, const uint32_t* seg_off, int64_t total,
+                          int k, float* D, int64_t* I, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,10 @@ def _random_index(idx_cls, rng, d, nlist, m, nbits, n, nonneg_ids=True):
     (64, 32, 16, 6, 8000, 33, 16, 4),
     (48, 8, 4, 12, 3000, 17, 32, 2),
     (1968, 8, 48, 12, 4000, 12, 10, 1),          # the reference's sub-quantiser shape
+    # any k (faiss's range): every probed row keyed and sorted per query (ivfpq_scan_all_device)
+    (32, 16, 8, 8, 5000, 40, 100, 1),
+    (64, 32, 16, 6, 8000, 33, 700, 4),
+    (1968, 8, 48, 12, 4000, 5, 2000, 2),
 ])
 def test_scan_matches_oracle_on_the_same_codes(gpu, d, nlist, m, nbits, n, nq, k, nprobe):
     from image_recommender_amd.ivfpq import IndexIVFPQ
@@ -79,6 +83,14 @@ def test_duplicate_codes_tie_by_label_and_short_lists_pad(gpu):
     idx.nprobe = 4
     D, I = idx.search(cen[:1] + 0.01, 10)
     assert sorted(I[0, :8].tolist()) == sorted(ids.tolist()) and (I[0, 8:] == -1).all()
+    # the same through the any-k route (k > 32): identical ranks, longer padding
+    D2, I2 = idx.search(cen[:1] + 0.01, 40)
+    np.testing.assert_array_equal(I2[0, :10], I[0])
+    np.testing.assert_array_equal(D2[0, :8], D[0, :8])
+    assert (I2[0, 8:] == -1).all() and (D2[0, 8:] == np.finfo(np.float32).max).all()
+    idx.nprobe = 1
+    D3, I3 = idx.search(cen[:1] + 0.01, 33)
+    assert I3[0, :6].tolist() == [2, 7, 12, 31, 50, 99] and (I3[0, 6:] == -1).all()
 
 
 def test_train_add_search_end_to_end(gpu):
@@ -121,8 +133,8 @@ def test_rejects_bad_shapes(gpu):
     idx.set_trained(np.zeros((4, 16), np.float32), np.zeros((4, 16, 4), np.float32))
     with pytest.raises(ValueError):
         idx.add_encoded([0], [[0, 0, 0, 16]], [0])
-    with pytest.raises(NotImplementedError):
-        idx.search(np.zeros((1, 16), np.float32), 33)
+    with pytest.raises(ValueError):
+        idx.search(np.zeros((1, 16), np.float32), 0)
 
 
 def test_write_read_roundtrip(gpu, tmp_path):
