@@ -202,9 +202,11 @@ hipError_t launch_ivfpq_scan_all(const float* lut, const int64_t* probes, int64_
             if (e == hipSuccess)
                 e = sort_u64_segments(a, b, total, (int)nq, seg_off, 64u, &tmp, &tmp_cap, true, st);
         }
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(ivfpq_write_all_kernel, dim3((unsigned)((k + 255) / 256), (unsigned)nq), dim3(256),
-                               0, st, b, seg_off, k, D, I);
+        // (queries in slices of 65535: the grid's y extent)
+        for (int64_t q0 = 0; q0 < nq && e == hipSuccess; q0 += 65535) {
+            const int64_t qn = std::min<int64_t>(65535, nq - q0);
+            hipLaunchKernelGGL(ivfpq_write_all_kernel, dim3((unsigned)((k + 255) / 256), (unsigned)qn), dim3(256),
+                               0, st, b, seg_off + q0, k, D + q0 * k, I + q0 * k);
             e = hipGetLastError();
         }
     }

@@ -35,6 +35,7 @@ namespace {
 constexpr int kHKT = 64;                       // rows and queries per key tile
 constexpr int kHKBK = 16;                      // k depth of one LDS stage
 constexpr int64_t kHKEntries = int64_t(1) << 27;   // keys per chunk (1 GiB of u64)
+constexpr int64_t kHKMaxQ = 65535;                 // queries per chunk: the write grid's y extent
 
 // keys[qi * nrows + row] for queries [0, nqc) of the padded query block qp (rows of dp floats,
 // zero beyond d) and every row of the index.  dp % 16 == 0 (knn_index rows are padded so).
@@ -188,7 +189,7 @@ int hugek_search(knn_index* ix, const float* q, int64_t nq, int k, float* D, int
         return KNN_OK;
     }
     if (ix->dp % kHKBK) KNN_FAIL(KNN_EINVAL, "row stride %d not a multiple of %d", ix->dp, kHKBK);
-    const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nq, kHKEntries / N));   // queries per chunk
+    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({nq, kHKEntries / N, kHKMaxQ}));   // queries per chunk
     const int64_t per_pad = round_up(per, kHKT);
     int rc;
     if ((rc = grow(&ix->qpad, &ix->qpad_cap, (size_t)per_pad * ix->dp)) != KNN_OK) return rc;
@@ -231,7 +232,7 @@ hipError_t launch_merge_huge(const float* cD, const int64_t* cI, int nlists, int
                              hipStream_t st) {
     if (nq <= 0) return hipSuccess;
     const int64_t M = (int64_t)nlists * kin;
-    const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nq, kHKEntries / std::max<int64_t>(M, 1)));
+    const int64_t per = std::max<int64_t>(1, std::min<int64_t>({nq, kHKEntries / std::max<int64_t>(M, 1), kHKMaxQ}));
     uint64_t *a = nullptr, *b = nullptr;
     unsigned* off = nullptr;
     void* tmp = nullptr;
