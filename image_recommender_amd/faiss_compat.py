@@ -44,7 +44,7 @@ from types import SimpleNamespace
 import numpy as np
 
 from . import _lib
-from ._lib import KNN_MAX_K, KNN_MAX_K_LARGE, KnnError
+from ._lib import KNN_MAX_K, KnnError
 
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
