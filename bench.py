@@ -404,7 +404,10 @@ def main():
     profiled = any(k.startswith("ROCPROF") for k in os.environ)
     if (a.pmc == "auto" and a.gpus == 1 and "WORLD_SIZE" not in os.environ and not a.profile_only
             and a.config in (2, 3) and not profiled):
-        live = live_pmc(a)
+        try:
+            live = live_pmc(a)
+        except Exception as e:          # an unexpected profiler output never costs the bench line
+            live = ({}, f"live PMC failed: {type(e).__name__}: {e}")
         print(f"[bench] live PMC: {live[1]}", file=sys.stderr, flush=True)
     # --gpus N > 1 without torchrun: start the N ranks here (no device touched in this process)
     # or stop with a non-zero status; never a silent one-GPU run (image_recommender_amd/launch.py)
