@@ -434,3 +434,21 @@ def test_cfg4_whole_10m_corpus_eight_shards(faiss):
     assert hits / (K * len(sel)) == 1.0, hits                    # recall@10, every query
     del idx
     torch.cuda.synchronize()
+
+
+def test_cfg3_full_size_any_k(faiss, cfg3):
+    """k = 2048 (> KNN_MAX_K_LARGE: csrc/knn_hugek.hip, every key + a segmented sort) on the whole
+    1M x 1968 cfg3 corpus for 4 queries, against the device float64 oracle of the same rows:
+    labels integer-exact at every rank separated by more than the empirical window.
+    /root/reference/main/search_from_image.py:27 (top_k), :247 (index.search)."""
+    import torch
+    from tests.device_oracle import device_topk
+    k, sel = 2048, np.array([0, 333, 700, 1023])
+    idx, xb = cfg3["idx"], cfg3["xb"]
+    D, I = idx.search(cfg3["xq"][sel], k)
+    assert D.shape == (len(sel), k) and (I >= 0).all() and (np.diff(D, axis=1) >= 0).all()
+    blocks = (torch.from_numpy(xb[i:i + 16384]).cuda() for i in range(0, xb.shape[0], 16384))
+    Dg, Ig, _, blas = device_topk(torch, blocks, cfg3["q"][sel].contiguous(), k + 1)
+    check_knn(D, I, xb, cfg3["xq"][sel], k, "l2", min_exact_frac=0.0, oracle=(Dg, Ig), tight=False)
+    check_knn_tight(D, I, xb, cfg3["xq"][sel], k, "l2", oracle=(Dg, Ig), blas=blas,
+                    min_rank_frac=0.75, min_set_frac=0.75, tag="cfg3 k=2048, 1M rows")
