@@ -71,6 +71,13 @@ hugek_keys_kernel(const float* __restrict__ xb, const float* __restrict__ xn, in
             a = xrow < nrows ? xs[s] : zero;
             b = qrow < nqc ? qs[s] : zero;
         }
+        // two-level sum: a stage's 16 products in their own chain, then added to the total (the
+        // error of a 1968-term key grows with ~124 + 16 additions instead of 1968)
+        float part[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) part[i][j] = 0.f;
 #pragma unroll
         for (int kk = 0; kk < kHKBK; ++kk) {
             const float4 xv = *reinterpret_cast<const float4*>(&sx[kk][tr * 4]);
@@ -79,8 +86,12 @@ hugek_keys_kernel(const float* __restrict__ xb, const float* __restrict__ xn, in
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xa[i], qa[j], acc[i][j]);
+                for (int j = 0; j < 4; ++j) part[i][j] = fmaf(xa[i], qa[j], part[i][j]);
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] += part[i][j];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -450,8 +450,9 @@ def test_cfg3_full_size_any_k(faiss, cfg3):
     blocks = (torch.from_numpy(xb[i:i + 16384]).cuda() for i in range(0, xb.shape[0], 16384))
     Dg, Ig, _, blas = device_topk(torch, blocks, cfg3["q"][sel].contiguous(), k + 1)
     check_knn(D, I, xb, cfg3["xq"][sel], k, "l2", min_exact_frac=0.0, oracle=(Dg, Ig), tight=False)
-    # (2,048 deep among 1M rows the neighbours' keys are packed within ~2e-5 of each other — the
-    # window of this route's sequential fp32 dot products — so ~30 % of the ranks are separated
-    # by more than it (measured 0.30); every one of those must carry the oracle's label)
+    # (2,048 deep among 1M rows the neighbours' keys are packed within a few 1e-6 of each other,
+    # the window of this route's fp32 dot products (16-term stage sums added to a running total),
+    # so only part of the ranks are separated by more (measured 0.69); every one of those must
+    # carry the oracle's label)
     check_knn_tight(D, I, xb, cfg3["xq"][sel], k, "l2", oracle=(Dg, Ig), blas=blas,
-                    min_rank_frac=0.2, min_set_frac=0.0, tag="cfg3 k=2048, 1M rows")
+                    min_rank_frac=0.5, min_set_frac=0.0, tag="cfg3 k=2048, 1M rows")
