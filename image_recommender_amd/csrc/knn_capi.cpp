@@ -285,6 +285,11 @@ int create_single(int d, int metric, int device, knn_index** out) {
         const int v = std::atoi(e);
         ix->i8_half_k = v >= 2 ? v : 0;
     }
+    if (const char* e = test_knob("IMGREC_I8_POOL")) {
+        ix->i8_pool64 = std::min(64, std::max(0, std::atoi(e)));
+        ix->i8_pool_forced = true;
+    }
+    if (const char* e = test_knob("IMGREC_I8_POOL_CH")) ix->i8_pool_ch = std::min(64, std::max(1, std::atoi(e)));
     if (const char* e = test_knob("IMGREC_DIRECT_RAW")) ix->direct_raw = std::min(2, std::max(0, std::atoi(e)));
     if (const char* e = test_knob("IMGREC_I8_FUSED_PREP")) ix->i8_fused_prep = *e != '0';
     if (const char* e = test_knob("IMGREC_RERANK_P1")) ix->rerank_p1k = *e != '0';
@@ -314,7 +319,7 @@ void free_single(knn_index* ix) {
                     (void*)ix->mws_f, (void*)ix->stat, (void*)ix->fb_cd, (void*)ix->fb_ci,
                     (void*)ix->b16_sync,
                     (void*)ix->tail_ctl, (void*)ix->chance, (void*)ix->sc_key, (void*)ix->sc_lab,
-                    (void*)ix->sc_meta, (void*)ix->sc_done, (void*)ix->heads})
+                    (void*)ix->sc_meta, (void*)ix->sc_done, (void*)ix->heads, (void*)ix->i8_dyn})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)ix->xb, (void*)ix->xn, (void*)ix->xs, (void*)ix->xn_max,
                     (void*)ix->qpad, (void*)ix->qnorm, (void*)ix->cand_d, (void*)ix->cand_i,

@@ -287,7 +287,7 @@ __device__ __forceinline__ void insert_mono(float (&kd)[K], int (&ki)[K], float 
     ki[0] = c[0] ? id : ki[0];
 }
 
-template <int NQ, int KM, int NBI>
+template <int NQ, int KM, int NBI, bool DYN>
 __global__ void __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(2)))
 knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ scales,
                    const float* __restrict__ xnorm, int nrows, int nblk,
@@ -297,7 +297,8 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
                    int64_t* __restrict__ cand_i, int ncand, const float* __restrict__ qsrc, int d,
                    int dp, int normalize, float* __restrict__ qpad, float* __restrict__ qnorm_out,
                    float* __restrict__ qresid, int* __restrict__ zero_ctl,
-                   float* __restrict__ heads, int raw16, int half_k) {
+                   float* __restrict__ heads, int raw16, int half_k, int* __restrict__ dyn,
+                   int pool, int pool_ch) {
     // the queries' two-level codes in LDS: block b of query q at sqc[q][b] = 64 hi codes | 64 lo
     // codes | 16-B pad — the pad puts lane j's block (b = j + 16 bi) on 16-B bank slot j, so a
     // ds_read_b128 lane group (16 distinct j) is conflict-free; their scales (s_hi, s_lo) in sqs
@@ -329,6 +330,10 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     const bool owner = j < NQ && j < nq;
 
     const int ngroups = (nrows + kGroup - 1) / kGroup;
+    // pool > 0 (I8Args::pool): the last `pool` groups are not assigned up front; a wave that has
+    // run out of its own groups takes chunks of pool_ch of them from the counter dyn[0], so the
+    // workgroups end together instead of the slowest 15-25 us behind the median
+    const int sg = DYN ? ngroups - pool : ngroups;               // statically assigned groups
     // H rows per lane and step: a wave step covers 4 H rows (H = 2: a whole 8-row group; H = 1 at
     // NQ = 8, at NQ = 4 with KM = 32 and at d > 2048: half a group, which keeps the queries'
     // dots, the lists and the prefetched codes within the register file — a spill's reload waits
@@ -341,11 +346,11 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     // first and ended ~10 us later (profiles/r05/i8_stamps/, loop_end_by_half)
     const int h2 = nsplit / 2;
     const bool first_half = split < h2;
-    const int rs = split < ngroups ? (ngroups - split + nsplit - 1) / nsplit : 0;    // own rounds
+    const int rs = split < sg ? (sg - split + nsplit - 1) / nsplit : 0;    // own rounds
     int ng = rs;
     if (half_k > 0) {
         if (first_half) {
-            const int rp = split + h2 < ngroups ? (ngroups - split - h2 + nsplit - 1) / nsplit : 0;
+            const int rp = split + h2 < sg ? (sg - split - h2 + nsplit - 1) / nsplit : 0;
             ng = rs + rp / half_k;
         } else {
             ng = rs - rs / half_k;
@@ -371,8 +376,9 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
         float xn[H];
         int row[H];
     };
-    auto load = [&](int li, Grp& G) __attribute__((always_inline)) {
-        const int m = group_of(li / kSub), r0 = m * kGroup + 4 * (li % kSub);
+    // sub-step sub of 8-row group m
+    auto load = [&](int m, int sub, Grp& G) __attribute__((always_inline)) {
+        const int r0 = m * kGroup + 4 * sub;
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             G.row[h] = r0 + 4 * h + g;
@@ -606,17 +612,92 @@ knn_i8_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ s
     // (the first group's loads issued before the query prep instead — by every wave, or only by
     // the waves that quantise no query — measured the same: profiles/r05/nq1/preload/)
     if (wave == 0) I8_STAMP(1);
-    if (li < cnt) load(li, A);
     bool first_done = false;
+    if constexpr (!DYN) {
+    if (li < cnt) load(group_of(li / kSub), li % kSub, A);
     while (li < cnt) {
-        if (li + kWaves < cnt) load(li + kWaves, B);
+        if (li + kWaves < cnt) load(group_of((li + kWaves) / kSub), (li + kWaves) % kSub, B);
         process(A);
         if (wave == 0 && !first_done) { I8_STAMP(2); first_done = true; }
         li += kWaves;
         if (li >= cnt) break;
-        if (li + kWaves < cnt) load(li + kWaves, A);
+        if (li + kWaves < cnt) load(group_of((li + kWaves) / kSub), (li + kWaves) % kSub, A);
         process(B);
         li += kWaves;
+    }
+    } else {
+    // The wave's steps in increasing row order (the lists' insert_mono needs it): its own
+    // groups' steps li = wave, wave + 4, ..., then the pool's chunks in the order the counter
+    // hands them out.  A chunk is 4 pool_ch groups for the whole workgroup (group c of the chunk
+    // to wave c % 4): wave 0 takes it with one lane's atomic add — issued a chunk ahead, so its
+    // latency hides under the products — and hands it over in LDS between two barriers (device
+    // atomics run beyond the XCD's L2: one per wave and group cost more than the imbalance,
+    // profiles/r06/i8_pool/).  The last workgroup to find the pool empty resets both counters
+    // for the next launch (no host zeroing; safe to replay in a graph).
+    __shared__ int s_chunk;
+    const int chw = 4 * pool_ch;                                 // groups per chunk
+    const int pool_chunks = pool > 0 ? (pool + chw - 1) / chw : 0;
+    int pend = 0;                       // wave 0, lane 0: the grab in flight
+    bool pend_on = false;
+    int pc_base = 0, pc_t = 0, pc_n = 0;    // this wave's share of the current chunk
+    auto grab = [&]() __attribute__((always_inline)) {
+        if (lane == 0) pend = __hip_atomic_fetch_add(dyn, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend_on = true;
+    };
+    auto fetch = [&]() __attribute__((always_inline)) -> int {
+        // (LDS only: the loads of the group in flight stay in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (wave == 0) {
+            if (!pend_on) grab();
+            const int p = __builtin_amdgcn_readfirstlane(pend);
+            pend_on = false;
+            if (lane == 0) s_chunk = p;
+            if (p < pool_chunks) {
+                grab();
+            } else if (lane == 0) {
+                const int n = __hip_atomic_fetch_add(dyn + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (n == (int)gridDim.x - 1) {
+                    __hip_atomic_store(dyn, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(dyn + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        return __builtin_amdgcn_readfirstlane(s_chunk);
+    };
+    auto next_step = [&]() __attribute__((always_inline)) -> int {
+        if (li < cnt) {
+            const int r = group_of(li / kSub) * kSub + li % kSub;
+            li += kWaves;
+            if (wave == 0 && pool_chunks > 0 && !pend_on && li + kWaves >= cnt) grab();
+            return r;
+        }
+        if (pool_chunks == 0) return -1;
+        for (;;) {
+            if (pc_t < pc_n) {
+                const int t = pc_t++;
+                return (pc_base + kWaves * (t / kSub)) * kSub + t % kSub;
+            }
+            const int p = fetch();                   // every wave of the workgroup, together
+            if (p >= pool_chunks) return -1;
+            pc_base = sg + p * chw + wave;
+            const int left = ngroups - pc_base;      // this wave's groups: pc_base + 4 i < ngroups
+            pc_n = kSub * (left <= 0 ? 0 : min(pool_ch, (left + kWaves - 1) / kWaves));
+            pc_t = 0;
+        }
+    };
+    int cur = next_step();
+    if (cur >= 0) load(cur / kSub, cur % kSub, A);
+    while (cur >= 0) {
+        const int nx = next_step();
+        if (nx >= 0) load(nx / kSub, nx % kSub, B);
+        process(A);
+        if (wave == 0 && !first_done) { I8_STAMP(2); first_done = true; }
+        if (nx < 0) break;
+        cur = next_step();
+        if (cur >= 0) load(cur / kSub, cur % kSub, A);
+        process(B);
+    }
     }
 
     I8_STAMP(3 + wave);
@@ -759,14 +840,25 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
     if (a.qsrc && a.nq > 4) return hipErrorInvalidValue;
     if (a.raw16 && (a.nq > 4 || a.ncand < a.nsplit * 16 * a.km)) return hipErrorInvalidValue;
     if (a.half_k != 0 && (a.half_k < 2 || a.nsplit % 2 != 0)) return hipErrorInvalidValue;
+    if (a.pool < 0 || a.pool > (a.nrows + kGroup - 1) / kGroup || a.pool_ch < 1 ||
+        (a.pool > 0 && (!a.dyn || a.half_k != 0)))
+        return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nsplit), block(kWaves * 64);
     const int nbi = (a.nblk + 15) / 16;
+    // the run-time pool is built for one or two queries with lists of 16 (the reference CLI's one
+    // query per search); other instances keep the static split (their registers have no room)
+    const bool dyn = a.pool > 0;
+    if (dyn && (a.nq > 2 || a.km != 16)) return hipErrorInvalidValue;
 #define IMGREC_I8(NQV, KMV, NBIV)                                                                 \
-    hipLaunchKernelGGL((knn_i8_scan_kernel<NQV, KMV, NBIV>), grid, block, 0, st, a.codes, a.scales, \
+    if (dyn) IMGREC_I8D(NQV, KMV, NBIV, (NQV <= 2 && KMV == 16));                                    \
+    else IMGREC_I8D(NQV, KMV, NBIV, false)
+#define IMGREC_I8D(NQV, KMV, NBIV, DYNV)                                                          \
+    hipLaunchKernelGGL((knn_i8_scan_kernel<NQV, KMV, NBIV, DYNV>), grid, block, 0, st, a.codes, a.scales, \
                        a.xnorm, a.nrows, a.nblk, a.qcodes, a.qscales, a.qnorm, a.nq, a.nsplit,      \
                        a.id_offset,                                                                 \
                        a.l2, a.cand_d, a.cand_i, a.ncand, a.qsrc, a.d, a.dp, a.normalize, a.qpad,  \
-                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads, a.raw16, a.half_k)
+                       a.qnorm_out, a.qresid, a.zero_ctl, a.heads, a.raw16, a.half_k, a.dyn,     \
+                       a.pool, a.pool_ch)
 #define IMGREC_I8_NBI(NQV, KMV)                                   \
     do {                                                          \
         switch (nbi) {                                            \
@@ -790,6 +882,7 @@ hipError_t launch_i8_scan(const I8Args& a, hipStream_t st) {
 #undef IMGREC_I8_KM
 #undef IMGREC_I8_NBI
 #undef IMGREC_I8
+#undef IMGREC_I8D
     return hipGetLastError();
 }
 

@@ -115,6 +115,15 @@ struct knn_index {
     // to the first half (I8Args::half_k; IMGREC_I8_HALF_K=K, 0 = even split).  12: config 2 one
     // query 0.1517 -> 0.1503 ms; 6-8 and 24-32 measured worse (profiles/r05/nq1/half_k/)
     int i8_half_k = 12;
+    // int8 scan: the last i8_pool64 / 64 of the row groups handed out at run time in chunks of
+    // 4 i8_pool_ch groups (I8Args::pool).  Default: one query on one workgroup per CU (rows of
+    // >= 24 blocks), where 4/64 in chunks of 8 groups took the config-3 search from 0.3258 to
+    // 0.3210 ms; config 2's two workgroups per CU lost 4-30 us with any pool (profiles/r06/i8_pool/).
+    // IMGREC_I8_POOL=<64ths> (0 = off) applies it to every one- or two-query scan with lists of 16.
+    int i8_pool64 = 4;
+    int i8_pool_ch = 2;
+    bool i8_pool_forced = false;
+    int* i8_dyn = nullptr;      // the pool's two counters (zeroed once; the scan leaves them at 0)
     bool stream_lists = true;   // exact lists of <= 4 queries from one fp32 stream (IMGREC_STREAM_LISTS=0: tiles)
     bool merge_single = false;  // IMGREC_MERGE_SINGLE=1: the single-level merge in the rerank
     bool rerank_nw4 = false;    // IMGREC_RERANK_NW4=1: large batches rerank on 4-wave workgroups

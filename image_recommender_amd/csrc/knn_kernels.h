@@ -233,6 +233,11 @@ struct I8Args {
     // > 1: every half_k-th round of row groups, a second-half split's group goes to split -
     // nsplit / 2 (two workgroups per CU: the one dispatched second gets less work); 0 = even
     int half_k = 0;
+    // > 0: the last `pool` 8-row groups are handed out at run time in chunks of pool_ch groups
+    // from the counter dyn[0] (dyn[1] counts the waves done; the scan leaves both at 0, so they
+    // are zeroed once when allocated); requires half_k = 0, nq <= 2 and km = 16
+    int* dyn = nullptr;
+    int pool = 0, pool_ch = 1;
 };
 // Bytes per row of the int8 copy: 64 per block, no padding (round 4; rows were whole 1-KiB
 // groups of 16 blocks, 25 % zeros at d = 768).  Blocks sit in groups of 16 (the scan's 16 lanes of

@@ -354,6 +354,18 @@ int i8_chunk(knn_index* ix, const float* qraw, const float* qpad, const float* q
     a.nsplit = p.nsplit; a.l2 = kmetric; a.id_offset = ix->id_offset; a.cand_d = ix->cand_d;
     a.cand_i = ix->cand_i; a.ncand = ncand; a.raw16 = raw ? 1 : 0;
     if (p.nsplit == 2 * ix->cus) a.half_k = ix->i8_half_k;     // two workgroups per CU
+    if (ix->i8_pool64 > 0 && nq <= 2 && p.km == 16 &&
+        (ix->i8_pool_forced || (nq == 1 && p.nsplit == ix->cus))) {
+        // run-time pool of the last row groups (I8Args::pool): replaces the half_k shift
+        if (!ix->i8_dyn) {
+            KNN_HIP(hipMalloc((void**)&ix->i8_dyn, 2 * sizeof(int)));
+            KNN_HIP(hipMemsetAsync(ix->i8_dyn, 0, 2 * sizeof(int), st));
+        }
+        a.dyn = ix->i8_dyn;
+        a.pool = (int)((ix->ntotal + 7) / 8 * ix->i8_pool64 / 64);
+        a.pool_ch = ix->i8_pool_ch;
+        a.half_k = 0;
+    }
     if (direct) {
         if ((rc = grow(&ix->tail_ctl, &ix->tail_ctl_cap, (size_t)4 + round_up(nq, 32) / 32)) != KNN_OK)
             return rc;

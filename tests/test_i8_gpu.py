@@ -378,3 +378,40 @@ def test_i8_weighted_halves_match_the_even_split(faiss, monkeypatch, d, metric):
                     assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), (name, rep, nq)
                 if rep == 0:
                     check_knn(D1, I1, xb, q, 10, metric, min_exact_frac=0.5)
+
+
+@pytest.mark.parametrize("d", [768, 1968])
+@pytest.mark.parametrize("metric", ["l2", "cosine"])
+def test_i8_group_pool_matches_the_static_split(faiss, monkeypatch, d, metric):
+    """The scan's run-time pool (I8Args::pool, round 6): the last row groups handed out in chunks
+    by a device counter that the scan resets itself.  Every returned bit equals the static split's
+    — pool off, the default 4/64, and everything pooled in the smallest chunks (64/64, one group
+    per wave) — over a ragged corpus (40,003 and 100,003 rows), one and two queries, search after
+    search (a counter left non-zero would skip rows on the next search)."""
+    xq = mixture(2, d, centres=40, seed=d + 52)
+    for n in (40003, 100003):
+        xb = mixture(n, d, centres=40, seed=d + n)
+        idx = {}
+        for name, pool, ch in (("off", "0", "2"), ("p4", "4", "2"), ("p64", "64", "1")):
+            monkeypatch.setenv("IMGREC_I8_POOL", pool)
+            monkeypatch.setenv("IMGREC_I8_POOL_CH", ch)
+            idx[name] = _index(faiss, d, metric)          # (the knobs are read at index creation)
+            monkeypatch.delenv("IMGREC_I8_POOL")
+            monkeypatch.delenv("IMGREC_I8_POOL_CH")
+            idx[name].add(xb)
+            idx[name].search_mode = "i8"
+        for rep in range(3):
+            for nq in (1, 2):
+                q = np.ascontiguousarray(xq[:nq])
+                D0, I0 = idx["off"].search(q, 10)
+                r0 = _stats(idx["off"], nq)
+                for name in ("p4", "p64"):
+                    D1, I1 = idx[name].search(q, 10)
+                    assert _lib().knn_last_path(idx[name].handle) == 3
+                    r1 = _stats(idx[name], nq)
+                    if r0 == 0 and r1 == 0:
+                        assert np.array_equal(I1, I0), (n, name, rep, nq, np.argwhere(I1 != I0)[:5])
+                        assert np.array_equal(D1.view(np.uint32), D0.view(np.uint32)), (n, name, rep, nq)
+                    if rep == 0:
+                        check_knn(D1, I1, xb, q, 10, metric, min_exact_frac=0.5 if d < 1024 else 0.25)
+        del idx
