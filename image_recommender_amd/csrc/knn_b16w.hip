@@ -194,6 +194,8 @@ __device__ __forceinline__ float bucket_end(uint32_t u, uint32_t lowmask) {
 #ifdef IMGREC_B16_STAMPS
 // diagnostic build only (tools/b16_stamps.py): s_memtime per wave at fixed points of one tile
 __device__ unsigned long long g_b16w_stamps[8 * 256];
+// per workgroup (blockIdx.x < 1024): s_memrealtime (100 MHz) at entry and after its last tile
+__device__ unsigned long long g_b16w_wg[2 * 1024];
 #define B16W_STAMP(slot) do { if (stamp_on && lane == 0) { \
     unsigned long long v_ = __builtin_amdgcn_s_memtime(); g_b16w_stamps[wave * 256 + (slot)] = v_; } } while (0)
 #else
@@ -213,6 +215,9 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
 
     // XCD-aware bijective block -> (query block, row split) map, as knn_b16_tile_kernel
     const int nwg = gridDim.x, wg = blockIdx.x;
+#ifdef IMGREC_B16_STAMPS
+    if (threadIdx.x == 0 && wg < 1024) g_b16w_wg[2 * wg] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int xcd = wg & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (wg >> 3);
     constexpr int kG = 4;
@@ -585,6 +590,9 @@ knn_b16w_tile_kernel(const uint32_t* __restrict__ xh, const float* __restrict__ 
         }
     }
 
+#ifdef IMGREC_B16_STAMPS
+    if (threadIdx.x == 0 && wg < 1024) g_b16w_wg[2 * wg + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     // ---- one list per (query, row split): fold lane quarters 2, 3 into 0, 1 (lane ^ 32), then
     // quarter 1 into 0 (lane ^ 16).  Entries a fold drops rank behind the folded list's last
     // entry, which the merge floor covers.
@@ -667,5 +675,8 @@ hipError_t launch_b16_wide(const TileArgs& a, hipStream_t st) {
 #ifdef IMGREC_B16_STAMPS
 extern "C" int knn_b16w_stamps_read(unsigned long long* host) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(imgrec::g_b16w_stamps), sizeof(imgrec::g_b16w_stamps));
+}
+extern "C" int knn_b16w_wg_read(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(imgrec::g_b16w_wg), sizeof(imgrec::g_b16w_wg));
 }
 #endif
